@@ -1,0 +1,285 @@
+#!/usr/bin/env python3
+"""bench.py -- CRC32C GiB/s, device-resident, batched 1 MiB blocks (BASELINE.json metric).
+
+One step = one pass of the CRC engine (libkvsep_crc32c, C ABI) over one batch that already sits in
+HBM: config 3 of BASELINE.json, 65,536 x 1 MiB blocks (64 GiB) per GPU (`--config 3a`, default);
+`--config 3b` is the vlog-framed variant (1,048,609-B payloads at 8 + i*(8+len): odd offsets),
+`2` is 65,536 x 4 KiB, `4` the Zipf ragged batch.  N > 1: one process per GPU (torchrun), each rank
+checksums its own shard (weak scaling, no data-path collective); rank 0 prints one JSON line.
+
+Outside the timed region: RCCL all-gather of each rank's CRC-of-CRCs digest, a parity spot check
+against the oracle (test infrastructure), the read-only streaming ceiling, the host round-trip rate
+and -- rank 0 at N = 1 -- the oracle's CPU throughput on a bounded sample (cpu_baseline).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "kv-separate_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import kvsep  # noqa: E402
+from kvsep import workloads as W  # noqa: E402
+
+GIB = float(1 << 30)
+HBM_PEAK_GBPS = 8000.0  # MI355X spec HBM3E peak (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def layout(cfg: str):
+    if cfg == "3a":
+        off, ln = W.cfg3_layout()
+        return off, ln, "65536 x 1 MiB blocks, 16-B aligned (config 3, variant A)"
+    if cfg == "3b":
+        off, ln = W.cfg3_layout(vlog=True)
+        return off, ln, "65536 x 1,048,609-B vlog payloads at 8 + i*(8+len) (config 3, variant B)"
+    if cfg == "2":
+        off, ln = W.cfg2_layout()
+        return off, ln, "65536 x 4 KiB SST blocks (config 2)"
+    if cfg == "4":
+        off, ln = W.cfg4_layout()
+        return off, ln, "1,048,576 Zipf(1.1) blocks, 32 B - 4 MiB (config 4)"
+    raise SystemExit(f"unknown config {cfg}")
+
+
+def to_dev_u64(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64)).to(dev)
+
+
+def load_oracle():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from conftest import load_oracle as _lo  # test infrastructure: the checker / CPU baseline only
+    return _lo()
+
+
+def cpu_baseline(oracle, data_dev, off, ln, sample_blocks, threads):
+    """Oracle (a restatement of util/crc32c.cc's portable path, compiled -O3) on host cores."""
+    idx = np.linspace(0, off.size - 1, sample_blocks).astype(np.int64)
+    lens = ln[idx]
+    host = np.empty(int(lens.sum()), dtype=np.uint8)
+    hoff = np.zeros(sample_blocks, dtype=np.uint64)
+    pos = 0
+    for k, i in enumerate(idx):  # gather the sampled blocks to host memory (untimed)
+        n = int(ln[i])
+        host[pos:pos + n] = data_dev[int(off[i]):int(off[i]) + n].cpu().numpy()
+        hoff[k] = pos
+        pos += n
+    out = {}
+    for t in sorted({1, threads}):
+        sub = sample_blocks if t > 1 else max(1, sample_blocks // 4)
+        sb = int(lens[:sub].sum())
+        oracle.batch(host, hoff[:min(sub, 8)], lens[:min(sub, 8)], threads=1)  # warm tables
+        t0 = time.perf_counter()
+        res = oracle.batch(host, hoff[:sub], lens[:sub], threads=t)
+        dt = time.perf_counter() - t0
+        out[t] = (sb / GIB / dt, sb, dt)
+    return out, host, hoff, lens, idx
+
+
+def host_roundtrip(ctx, nbytes_target: int):
+    """Pinned host vlog image -> H2D -> CRC kernel -> D2H of the u32 results (two streams)."""
+    off, ln = W.cfg3_layout(vlog=True, count=max(1, nbytes_target // (W.VLOG_PAYLOAD + 8)))
+    span = int(off[-1] + ln[-1])
+    buf = torch.empty(span, dtype=torch.uint8, pin_memory=True)
+    dev = torch.empty(span, dtype=torch.uint8, device="cuda")
+    kvsep.fill_splitmix64(dev.data_ptr(), span, 77, 0)
+    buf.copy_(dev)
+    torch.cuda.synchronize()
+    del dev
+    arr = buf.numpy()
+    ctx.batch_host_span(arr, off, ln)  # warm staging
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        res = ctx.batch_host_span(arr, off, ln)
+    dt = (time.perf_counter() - t0) / reps
+    return float(ln.sum()) / GIB / dt, int(ln.sum()), res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="3a", choices=["3a", "3b", "2", "4"])
+    ap.add_argument("--piece-kib", type=int, default=0, help="work-item size (0 = library default)")
+    ap.add_argument("--schedule", default="default", choices=["default", "static", "dynamic"])
+    ap.add_argument("--no-plan-hint", action="store_true", help="pass max_len = 0 (force the planning pass)")
+    ap.add_argument("--cpu-sample-blocks", type=int, default=4096)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--roundtrip-gib", type=float, default=4.0)
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    ctx = kvsep.Context(local)
+    if args.piece_kib:
+        ctx.set_piece_bytes(args.piece_kib * 1024)
+    if args.schedule != "default":
+        ctx.set_schedule(args.schedule == "dynamic")
+
+    off, ln, desc = layout(args.config)
+    count = int(off.size)
+    useful = int(ln.sum())
+    span = int(off[-1] + ln[-1])
+    max_len = 0 if args.no_plan_hint else int(ln.max())
+    log(f"[rank {rank}] {desc}: {useful / GIB:.2f} GiB useful, span {span / GIB:.2f} GiB")
+
+    # synthetic data, generated in HBM: rank r holds bytes [r*span, (r+1)*span) of one stream
+    data = torch.empty(span + 64, dtype=torch.uint8, device=dev)
+    seed = W.SEED + (1 if args.config.startswith("3") else 2 if args.config == "4" else 0)
+    kvsep.fill_splitmix64(data.data_ptr(), span, seed, rank * span)
+    d_off, d_len = to_dev_u64(off, dev), to_dev_u64(ln, dev)
+    out = torch.zeros(count, dtype=torch.int32, device=dev)
+    ctx.reserve(count, useful)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        ctx.batch_device(data.data_ptr(), d_off, d_len, out, count=count, total_bytes=useful, max_len=max_len,
+                         stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.get_timing()
+    ctx.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_timing(False)
+    kern_ms, launches = ctx.get_timing()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = world * useful * args.steps / GIB / elapsed
+    kern_avg_ms = kern_ms / max(1, launches)
+    achieved_gbps = useful / (kern_avg_ms * 1e-3) / 1e9
+
+    # ---- outside the timed region: result digest gather (RCCL), parity spot check, ceilings
+    crcs = out.cpu().numpy().view(np.uint32)
+    digest = kvsep.extend_host(0, crcs.tobytes())
+    digests = [digest]
+    if world > 1:
+        dt_ = torch.tensor([digest], dtype=torch.int64, device=dev)
+        gl = [torch.zeros_like(dt_) for _ in range(world)]
+        dist.all_gather(gl, dt_)
+        digests = [int(x.item()) for x in gl]
+
+    sink = torch.zeros(4, dtype=torch.int32, device=dev)
+    ctx.stream_read(data.data_ptr(), span, sink, stream=stream)  # warm
+    torch.cuda.synchronize()
+    ctx.set_timing(True)
+    for _ in range(3):
+        ctx.stream_read(data.data_ptr(), span, sink, stream=stream)
+    torch.cuda.synchronize()
+    ctx.set_timing(False)
+    sr_ms, sr_n = ctx.get_timing()
+    read_ceiling_gbps = (span // 16 * 16) / (sr_ms / sr_n * 1e-3) / 1e9
+
+    parity = None
+    cpu = None
+    if rank == 0:
+        oracle = load_oracle()
+        threads = min(args.cpu_threads, len(os.sched_getaffinity(0)))
+        nsample = min(args.cpu_sample_blocks, count)
+        if not args.no_cpu and world == 1:
+            res, host, hoff, lens, idx = cpu_baseline(oracle, data, off, ln, nsample, threads)
+            exp = oracle.batch(host, hoff, lens, threads=threads)
+            parity = bool(np.array_equal(exp, crcs[idx]))
+            vt, sbt, dtt = res[threads]
+            v1, sb1, dt1 = res[1]
+            cpu = {"value": round(vt, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+                   "sample": f"{nsample} blocks of the same batch ({sbt / GIB:.2f} GiB) copied to host memory, "
+                             f"oracle/crc32c_oracle.c (restated util/crc32c.cc portable path, gcc -O3), "
+                             f"{threads} threads split by bytes; 1 thread: {v1:.3f} GiB/s on {sb1 / GIB:.2f} GiB",
+                   "single_thread_GiBps": round(v1, 3)}
+        else:
+            idx = np.linspace(0, count - 1, 16).astype(np.int64)
+            hostb = [data[int(off[i]):int(off[i] + ln[i])].cpu().numpy() for i in idx]
+            exp = [oracle.extend_addr(0, h.ctypes.data, h.size) for h in hostb]
+            parity = bool(list(crcs[idx]) == exp)
+
+    rt = None
+    if rank == 0 and world == 1 and args.roundtrip_gib > 0:
+        try:
+            rt_gibps, rt_bytes, _ = host_roundtrip(ctx, int(args.roundtrip_gib * GIB))
+            rt = round(rt_gibps, 3)
+        except Exception as e:  # keep the headline line even if pinned allocation is refused
+            log(f"host round trip failed: {e}")
+
+    traffic = None
+    if os.path.exists(args.pmc_json):
+        try:
+            pm = json.load(open(args.pmc_json))
+            if pm.get("config") == args.config:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        line = {
+            "metric": "CRC32C GiB/s device-resident, batched 1 MiB blocks, 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64 byte stream generated in HBM)",
+            "config": {"workload": desc, "config": args.config, "blocks_per_gpu": count,
+                       "bytes_per_gpu": useful, "piece_bytes": args.piece_kib * 1024 or 256 * 1024,
+                       "parallelism": f"shard{world} (independent blocks per GPU, no data-path collective)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved_gbps / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                         "kernel": "crc32c_pieces_kernel", "kernel_avg_ms": round(kern_avg_ms, 4),
+                         "algorithmic_bytes_per_launch": useful},
+            "cpu_baseline": cpu,
+            "read_ceiling_GBps": round(read_ceiling_gbps, 1),
+            "frac_of_read_ceiling": round(achieved_gbps / read_ceiling_gbps, 4),
+            "host_roundtrip_GiBps": rt,
+            "parity_spot_check": parity,
+            "digests": [hex(d) for d in digests],
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,112 @@
+/*
+ * kvsep_crc32c.h -- C ABI of the MI355X-native CRC-32C-over-blocks engine (libkvsep_crc32c.so).
+ *
+ * Drop-in boundary for the checksum hot path of Buildings-Lei/kv-separate:
+ *   util/crc32c.h:17   uint32_t leveldb::crc32c::Extend(uint32_t init_crc, const char* data, size_t n)
+ *   util/crc32c.h:20   Value(data, n) = Extend(0, data, n)
+ *   util/crc32c.h:22-38 kMaskDelta / Mask / Unmask
+ *   port/port_stdcxx.h:142-152  port::AcceleratedCRC32C(crc, buf, size)  -- the reference's own
+ *                      plug point for an accelerated backend (self-test util/crc32c.cc:267-274)
+ * plus batched entry points that the reference's call sites would bind to when they hold a batch
+ * of independent records/blocks:
+ *   db/value_log_reader.cc:86-138  vlog record verify (recovery db/db_impl.cc:485-571, GC :880-951)
+ *   db/value_log_writer.cc:46-76   vlog record checksum before Append
+ *   table/table_builder.cc:209-232, table/format.cc:99-108  SST block trailers
+ *   db/log_writer.cc:84-115, db/log_reader.cc:246-259  MANIFEST fragments (per-type init CRC)
+ *
+ * All pointers are plain; no framework types cross this boundary.  Results are bit-exact with
+ * util/crc32c.cc (checked by tests/ against golden vectors captured from the compiled reference).
+ */
+#ifndef KVSEP_CRC32C_H_
+#define KVSEP_CRC32C_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KVSEP_OK 0
+#define KVSEP_EINVAL (-1)  /* bad argument */
+#define KVSEP_EHIP (-2)    /* a HIP runtime call failed (message via kvsep_last_error) */
+#define KVSEP_ENODEV (-3)  /* no usable gfx950 device */
+#define KVSEP_ENOMEM (-4)  /* device or pinned allocation failed */
+
+/* ---------------------------------------------------------------- scalar drop-in
+ * Same contract as util/crc32c.h:17 / util/crc32c.cc:276: CRC-32C of A||data[0,n) where
+ * init_crc = crc32c(A); n == 0 returns init_crc; any alignment; never fails; reentrant.
+ * Dispatch: n >= the offload threshold (kvsep_set_offload_threshold, default 64 MiB) goes through
+ * the GPU (pinned staging, H2D, kernel, D2H); smaller inputs use the host SSE4.2 path
+ * (the role google/crc32c plays behind port::AcceleratedCRC32C). */
+uint32_t kvsep_crc32c_extend(uint32_t init_crc, const char* data, size_t n);
+uint32_t kvsep_crc32c_value(const char* data, size_t n); /* util/crc32c.h:20 */
+uint32_t kvsep_crc32c_mask(uint32_t crc);                /* util/crc32c.h:29-32 */
+uint32_t kvsep_crc32c_unmask(uint32_t masked_crc);       /* util/crc32c.h:35-38 */
+/* port/port_stdcxx.h:142: returns Extend(crc, buf, size); never 0 for the self-test buffer. */
+uint32_t kvsep_accelerated_crc32c(uint32_t crc, const char* buf, size_t size);
+void kvsep_set_offload_threshold(uint64_t nbytes);
+/* Host-only CRC (SSE4.2 crc32 instructions, 3-way interleaved): the small-input leg of Extend. */
+uint32_t kvsep_crc32c_extend_host(uint32_t init_crc, const char* data, size_t n);
+
+/* ---------------------------------------------------------------- device context */
+typedef struct kvsep_crc32c_ctx kvsep_crc32c_ctx;
+
+int kvsep_crc32c_ctx_create(int device, kvsep_crc32c_ctx** out);
+void kvsep_crc32c_ctx_destroy(kvsep_crc32c_ctx* ctx);
+/* Work-item ("piece") size for splitting long blocks; default 256 KiB, min 1 KiB, multiple of 1 KiB. */
+int kvsep_crc32c_ctx_set_piece_bytes(kvsep_crc32c_ctx* ctx, uint64_t piece_bytes);
+/* 0 = static round-robin of pieces over waves, 1 = dynamic (atomic work counter). Default 1. */
+int kvsep_crc32c_ctx_set_schedule(kvsep_crc32c_ctx* ctx, int dynamic);
+/* Pre-size scratch so later calls of up to `count` blocks / `total_bytes` bytes do not allocate
+ * (required before graph capture). */
+int kvsep_crc32c_reserve(kvsep_crc32c_ctx* ctx, uint64_t count, uint64_t total_bytes);
+/* Kernel timing with HIP events on the caller's stream, around the main CRC kernel only. */
+int kvsep_crc32c_ctx_set_timing(kvsep_crc32c_ctx* ctx, int enable);
+int kvsep_crc32c_ctx_get_timing(kvsep_crc32c_ctx* ctx, double* total_ms, uint64_t* launches); /* syncs + resets */
+
+/* ---------------------------------------------------------------- batched device form
+ * out[i] = Extend(init ? init[i] : 0, base + off[i], len[i]) for i < count.
+ * base/off/len/init/out are DEVICE pointers; the call is asynchronous on `stream`
+ * (a hipStream_t; NULL = default stream).  Blocks may overlap and sit at any byte alignment.
+ * total_bytes >= sum(len) (sizes scratch only); max_len = an upper bound on len[i] or 0 if unknown
+ * (when max_len <= piece size the planning pass is skipped). */
+int kvsep_crc32c_batch_device(kvsep_crc32c_ctx* ctx, void* stream, const void* base, const uint64_t* off,
+                              const uint64_t* len, const uint32_t* init, uint32_t* out, uint64_t count,
+                              uint64_t total_bytes, uint64_t max_len);
+
+/* Verify form: as above, plus Mask(out[i]) is compared with expected_masked[i] (the stored LE32
+ * header word of db/value_log_writer.cc:58-59).  *first_bad (device) receives the lowest mismatching
+ * index or UINT64_MAX, *nbad the number of mismatches -- the reader truncates at the first bad
+ * record (db/value_log_reader.cc:112-122), so callers keep records [0, *first_bad). */
+int kvsep_crc32c_verify_device(kvsep_crc32c_ctx* ctx, void* stream, const void* base, const uint64_t* off,
+                               const uint64_t* len, const uint32_t* init, const uint32_t* expected_masked,
+                               uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count,
+                               uint64_t total_bytes, uint64_t max_len);
+
+/* ---------------------------------------------------------------- batched host form
+ * Host pointers.  Blocks are gathered into pinned staging, copied H2D, checksummed and the
+ * u32 results copied back, double-buffered over two streams; blocking. */
+int kvsep_crc32c_batch_host(kvsep_crc32c_ctx* ctx, const uint32_t* init, const char* const* ptr,
+                            const uint64_t* len, uint32_t* out, uint64_t count);
+/* One contiguous host buffer (a vlog file image or a block buffer headed for pwrite):
+ * out[i] = Extend(init?init[i]:0, host_base + off[i], len[i]). Blocking. */
+int kvsep_crc32c_batch_host_span(kvsep_crc32c_ctx* ctx, const char* host_base, uint64_t span_bytes,
+                                 const uint64_t* off, const uint64_t* len, const uint32_t* init, uint32_t* out,
+                                 uint64_t count);
+
+/* ---------------------------------------------------------------- support
+ * Synthetic data: byte i of the stream is byte (i&7) of splitmix64 word (i>>3) of `seed`
+ * (word j = mix(seed + (j+1)*0x9E3779B97F4A7C15)); writes bytes [stream_offset, +nbytes) to dst. */
+int kvsep_fill_splitmix64_device(void* stream, void* dst, uint64_t nbytes, uint64_t seed, uint64_t stream_offset);
+/* Read-only streaming kernel over [src, src+nbytes) (16-B loads, XOR-reduced into *sink):
+ * the attainable HBM-read ceiling the CRC kernel is compared with. */
+int kvsep_stream_read_device(kvsep_crc32c_ctx* ctx, void* stream, const void* src, uint64_t nbytes, uint32_t* sink);
+const char* kvsep_last_error(void);
+const char* kvsep_build_info(void);
+int kvsep_device_count(void);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+#endif /* KVSEP_CRC32C_H_ */

@@ -1,0 +1,726 @@
+// crc32c_device.hip -- CDNA4 (gfx950) kernels and the device-side C ABI of libkvsep_crc32c.
+//
+// Computes leveldb::crc32c::Extend (util/crc32c.cc:276-377) for batches of independent byte
+// blocks resident in HBM.  Design:
+//
+//  * Work item = "piece": a block, or an end-aligned slice of at most `piece_bytes` of a long block
+//    (pieces 1..k-1 are exactly piece_bytes long, piece 0 takes the remainder and the init CRC).
+//  * One wavefront per piece.  The piece is cut at 16-byte-aligned addresses into
+//      head  [ps, h0)   < 16 B, serial (word/byte steps),
+//      body  [h0, a1)   16-B aligned, as rows of 1 KiB ending exactly at a1,
+//      tail  [a1, pe)   < 16 B, serial.
+//    In the body every lane loads one 16-B vector per row (global_load_dwordx4, one 1 KiB
+//    coalesced wave-instruction per row) and owns four 32-bit "stride chains" -- the reference's
+//    4-stride swath (util/crc32c.cc:332-348) widened to 256 strides, 1 KiB apart:
+//        c' = word ^ Z_1024(c)
+//    Z_1024 is evaluated as 4 byte-table lookups in LDS.  The four tables are replicated 32x so that
+//    lane L always reads bank L%32: ds_read_b32 is conflict-free whatever the data.  The lookup
+//    address (table pair, byte value, lane copy) is assembled by ONE v_perm_b32 per lookup.
+//  * Chains are merged per lane with Z_4 (the STEP4W re-injection, util/crc32c.cc:307-315, 361-366),
+//    then across the 64 lanes by a 6-level butterfly with Z_16 .. Z_512 (DPP/bpermute shuffles).
+//  * Pieces of one block are merged by a tiny combine kernel: R(A||B) = Z_|B|(R(A)) ^ R(B).
+//
+// Every map Z_d ("advance the CRC register over d zero bytes") is generated on the host from the
+// Castagnoli polynomial (gf2.h); no table is copied from the reference.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/kvsep_crc32c.h"
+#include "gf2.h"
+#include "kvsep_internal.h"
+
+namespace kvsep {
+
+// ------------------------------------------------------------------------------------------------
+// LDS image of one CRC workgroup (bytes).  160,768 B of the 163,840 B a gfx950 workgroup may own.
+constexpr int kWgThreads = 1024;  // 16 waves: 4 per SIMD
+constexpr int kWavesPerWg = kWgThreads / 64;
+// [0, 128 KiB): Z_1024, 4 byte-tables x 256 entries x 32 lane copies (see fold1024)
+constexpr uint32_t kZ4Off = 131072;      // Z_4     (4 KiB)
+constexpr uint32_t kTreeOff = 135168;    // Z_16, Z_32, Z_64, Z_128, Z_256, Z_512 (6 x 4 KiB)
+constexpr uint32_t kByteOff = 159744;    // Z_1 low-byte table (1 KiB) = the STEP1 table
+constexpr uint32_t kLdsBytes = 160768;
+constexpr uint32_t kRowBytes = 1024;     // 64 lanes x 16 B
+
+struct DevTables {
+  uint32_t z1024[4][256];
+  uint32_t z4[4][256];      // kZ4Off
+  uint32_t ztree[6][4][256];// kTreeOff   (contiguous with z4 and byte1: copied to LDS as one run)
+  uint32_t byte1[256];      // kByteOff
+  uint32_t zpiece[4][256];  // Z_piece_bytes, used by the combine kernel
+};
+static_assert(sizeof(DevTables) == 4096 * 9 + 1024, "table layout");
+
+struct PiecesArgs {
+  const uint8_t* base;
+  const uint64_t* off;
+  const uint64_t* len;
+  const uint32_t* init;             // nullable -> 0
+  uint32_t* out;
+  const uint32_t* expect;           // nullable: verify mode
+  unsigned long long* first_bad;
+  unsigned long long* nbad;
+  uint64_t count;
+  const uint32_t* pstart;           // planned mode: piece range of block b = [pstart[b], pstart[b+1])
+  const uint32_t* pblk;             // planned mode: block of piece g
+  uint32_t* partial;                // planned mode: raw register of piece g
+  uint32_t* work_counter;           // dynamic schedule
+  uint64_t piece_bytes;
+  uint64_t max_pieces;              // capacity of pblk/partial
+  const DevTables* tabs;
+};
+
+__device__ __forceinline__ uint32_t lds_u32(const uint8_t* lds, uint32_t byte_off) {
+  return *reinterpret_cast<const uint32_t*>(lds + byte_off);
+}
+
+// Z_d through a plain (non-replicated) 4 KiB table set at byte offset t.
+__device__ __forceinline__ uint32_t zmap(const uint8_t* lds, uint32_t t, uint32_t w) {
+  return lds_u32(lds, t + ((w << 2) & 0x3fcu)) ^ lds_u32(lds, t + 1024u + ((w >> 6) & 0x3fcu)) ^
+         lds_u32(lds, t + 2048u + ((w >> 14) & 0x3fcu)) ^ lds_u32(lds, t + 3072u + ((w >> 22) & 0x3fcu));
+}
+
+// Z_1024 through the replicated tables.  Layout: byte addr = pair*64K + b*256 + half*128 + copy*4
+// with table k = 2*pair + half.  v_perm_b32 picks {copy*4 | b<<8 | pair<<16} in one instruction:
+//   sel byte0 = 0x00 -> lcX.byte0 (copy*4), byte1 = 0x04+k -> c.byte k, byte2 = 0x02 -> lcX.byte2 (pair),
+//   byte3 = 0x0C -> 0.
+__device__ __forceinline__ uint32_t fold1024(const uint8_t* lds, uint32_t c, uint32_t lc0, uint32_t lc1) {
+  const uint32_t a0 = __builtin_amdgcn_perm(c, lc0, 0x0C020400u);
+  const uint32_t a1 = __builtin_amdgcn_perm(c, lc0, 0x0C020500u);
+  const uint32_t a2 = __builtin_amdgcn_perm(c, lc1, 0x0C020600u);
+  const uint32_t a3 = __builtin_amdgcn_perm(c, lc1, 0x0C020700u);
+  return lds_u32(lds, a0) ^ lds_u32(lds, a1 + 128u) ^ lds_u32(lds, a2) ^ lds_u32(lds, a3 + 128u);
+}
+
+// Serial steps over bytes [q0, q1) of a 16-B aligned chunk (0 <= q0 <= q1 <= 16), wave-uniform.
+// Aligned whole words take one Z_4 step (util/crc32c.cc STEP4W), the rest byte steps (STEP1).
+__device__ __forceinline__ uint32_t serial16(const uint8_t* lds, uint32_t reg, uint4 ch, int q0, int q1) {
+  const uint32_t w[4] = {ch.x, ch.y, ch.z, ch.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int lo = 4 * k;
+    if (q0 <= lo && lo + 4 <= q1) {
+      reg = zmap(lds, kZ4Off, reg ^ w[k]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pos = lo + i;
+        if (pos >= q0 && pos < q1) {
+          const uint32_t b = (reg ^ (w[k] >> (8 * i))) & 0xffu;
+          reg = lds_u32(lds, kByteOff + (b << 2)) ^ (reg >> 8);
+        }
+      }
+    }
+  }
+  return reg;
+}
+
+// Global (not flat) address space: flat loads would tie the LDS counter to every data load.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4 gu32x4;
+__device__ __forceinline__ uint4 ld16(uintptr_t addr) {
+  const u32x4 v = *reinterpret_cast<gu32x4*>(addr);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// Raw CRC register after consuming [ps, pe) starting from register `reg` (no final inversion).
+__device__ __forceinline__ uint32_t crc_piece(const uint8_t* lds, uintptr_t ps, uintptr_t pe, uint32_t reg, uint32_t lane,
+                              uint32_t lc0, uint32_t lc1) {
+  const uintptr_t hbase = ps & ~uintptr_t(15);
+  uintptr_t h0 = (ps + 15) & ~uintptr_t(15);
+  if (h0 > pe) h0 = pe;
+  uintptr_t a1 = pe & ~uintptr_t(15);
+  if (a1 < h0) a1 = h0;
+
+  uint4 hc = make_uint4(0, 0, 0, 0), tc = make_uint4(0, 0, 0, 0);
+  if (ps < h0) hc = ld16(hbase);  // the aligned 16 B holding the head (never crosses a page)
+  if (a1 < pe) tc = ld16(a1);     // the aligned 16 B holding the tail
+
+  if (a1 > h0) {
+    const uint64_t K = (uint64_t(a1 - h0) + kRowBytes - 1) / kRowBytes;  // rows, the last ends at a1
+    const uintptr_t rb = a1 - K * kRowBytes;
+    const uintptr_t seg = rb + uintptr_t(lane) * 16u;
+    // issue the first rows' loads before the serial head work
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (seg >= h0) v = ld16(seg);  // row 0 is front-masked: lanes before h0 hold zeros
+    const uint64_t ngroups = (K - 1) >> 2;
+    uint4 A0, A1, A2, A3;
+    if (ngroups) {
+      A0 = ld16(seg + 1 * kRowBytes);
+      A1 = ld16(seg + 2 * kRowBytes);
+      A2 = ld16(seg + 3 * kRowBytes);
+      A3 = ld16(seg + 4 * kRowBytes);
+    }
+    if (ps < h0) reg = serial16(lds, reg, hc, int(ps - hbase), int(h0 - hbase));
+    if (seg == h0) v.x ^= reg;  // the head register enters as pending word at h0
+    uint32_t c0 = v.x, c1 = v.y, c2 = v.z, c3 = v.w;
+
+#define KVSEP_ROW(V)                                  \
+  do {                                                \
+    c0 = (V).x ^ fold1024(lds, c0, lc0, lc1);         \
+    c1 = (V).y ^ fold1024(lds, c1, lc0, lc1);         \
+    c2 = (V).z ^ fold1024(lds, c2, lc0, lc1);         \
+    c3 = (V).w ^ fold1024(lds, c3, lc0, lc1);         \
+  } while (0)
+
+    uint64_t r = 1;
+    const uint64_t last = K - 1;
+    for (uint64_t g = 0; g < ngroups; ++g) {
+      const uint64_t nr = r + 4;  // prefetch the next group (clamped: re-reads of the last row are harmless)
+      const uint4 B0 = ld16(seg + (nr + 0 < last ? nr + 0 : last) * kRowBytes);
+      const uint4 B1 = ld16(seg + (nr + 1 < last ? nr + 1 : last) * kRowBytes);
+      const uint4 B2 = ld16(seg + (nr + 2 < last ? nr + 2 : last) * kRowBytes);
+      const uint4 B3 = ld16(seg + (nr + 3 < last ? nr + 3 : last) * kRowBytes);
+      KVSEP_ROW(A0);
+      KVSEP_ROW(A1);
+      KVSEP_ROW(A2);
+      KVSEP_ROW(A3);
+      A0 = B0; A1 = B1; A2 = B2; A3 = B3;
+      r = nr;
+    }
+    for (; r < K; ++r) {
+      const uint4 V = ld16(seg + r * kRowBytes);
+      KVSEP_ROW(V);
+    }
+#undef KVSEP_ROW
+    // lane merge: pending word at (16*lane + 12) of the last row
+    uint32_t p = zmap(lds, kZ4Off, c0) ^ c1;
+    p = zmap(lds, kZ4Off, p) ^ c2;
+    p = zmap(lds, kZ4Off, p) ^ c3;
+    // butterfly over lanes: level j moves a 16*2^j-byte segment's pending word forward by 16*2^j
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const uint32_t o = __shfl_xor(p, 1 << j);
+      const uint32_t moved = zmap(lds, kTreeOff + 4096u * j, o) ^ p;
+      p = (lane & (1u << j)) ? moved : p;
+    }
+    p = __shfl(p, 63);               // pending word at a1 - 4
+    reg = zmap(lds, kZ4Off, p);      // register at a1
+  } else if (ps < h0) {
+    reg = serial16(lds, reg, hc, int(ps - hbase), int(h0 - hbase));
+  }
+  if (a1 < pe) reg = serial16(lds, reg, tc, 0, int(pe - a1));
+  return reg;
+}
+
+__device__ __forceinline__ uint32_t mask_crc(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xa282ead8u; }
+
+__device__ __forceinline__ void emit_block(const PiecesArgs& a, uint64_t b, uint32_t crc) {
+  a.out[b] = crc;
+  if (a.expect && mask_crc(crc) != a.expect[b]) {
+    atomicMin(a.first_bad, (unsigned long long)b);
+    atomicAdd(a.nbad, 1ull);
+  }
+}
+
+template <bool kPlanned, bool kDynamic>
+__global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+  const uint32_t tid = threadIdx.x;
+  // ---- fill LDS: replicated Z_1024 (coalesced dword stores), then the small tables as one run
+  {
+    uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
+    const uint32_t* z = &a.tabs->z1024[0][0];
+#pragma unroll 4
+    for (uint32_t i = 0; i < 32; ++i) {
+      const uint32_t idx = tid + i * kWgThreads;  // dword index in the replicated image
+      const uint32_t pair = idx >> 14, b = (idx >> 6) & 255u, half = (idx >> 5) & 1u;
+      l32[idx] = z[(2u * pair + half) * 256u + b];
+    }
+    const uint32_t* src = &a.tabs->z4[0][0];
+    for (uint32_t i = tid; i < (kLdsBytes - kZ4Off) / 4; i += kWgThreads) l32[kZ4Off / 4 + i] = src[i];
+  }
+  __syncthreads();
+
+  const uint32_t lane = tid & 63u;
+  const uint32_t lc0 = (lane & 31u) << 2;
+  const uint32_t lc1 = lc0 | 0x10000u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerWg;
+
+  uint64_t total = a.count;
+  if (kPlanned) {
+    total = a.pstart[a.count];
+    if (total > a.max_pieces) total = a.max_pieces;  // scratch overflow guard (caller bound violated)
+  }
+
+  uint64_t g;
+  if (kDynamic) {
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(a.work_counter, 1u);
+    g = __builtin_amdgcn_readfirstlane(t);
+  } else {
+    g = uint64_t(blockIdx.x) * kWavesPerWg + wave;
+  }
+
+  while (g < total) {
+    uint64_t gn;
+    if (kDynamic) {  // fetch the next ticket while this piece is processed
+      uint32_t t = 0;
+      if (lane == 0) t = atomicAdd(a.work_counter, 1u);
+      gn = __builtin_amdgcn_readfirstlane(t);
+    } else {
+      gn = g + nwaves;
+    }
+    uint64_t b;
+    uint64_t rs, re;
+    bool first, only;
+    const uint64_t n_b = 0;
+    (void)n_b;
+    if (kPlanned) {
+      b = a.pblk[g];
+      const uint64_t s = a.pstart[b], k = uint64_t(a.pstart[b + 1]) - s, j = g - s;
+      const uint64_t n = a.len[b];
+      re = n - (k - 1 - j) * a.piece_bytes;
+      rs = j ? n - (k - j) * a.piece_bytes : 0;
+      first = (j == 0);
+      only = (k == 1);
+    } else {
+      b = g;
+      rs = 0;
+      re = a.len[b];
+      first = true;
+      only = true;
+    }
+    const uintptr_t blk = reinterpret_cast<uintptr_t>(a.base) + a.off[b];
+    uint32_t reg0 = 0;
+    if (first) reg0 = ~(a.init ? a.init[b] : 0u);
+    const uint32_t reg = crc_piece(lds, blk + rs, blk + re, reg0, lane, lc0, lc1);
+    if (lane == 0) {
+      if (only) emit_block(a, b, ~reg);
+      else a.partial[g] = reg;
+    }
+    g = gn;
+  }
+}
+
+// One thread per block: Horner over the block's pieces, R <- Z_piece(R) ^ R_piece.
+__global__ void __launch_bounds__(256) crc32c_combine_kernel(PiecesArgs a) {
+  __shared__ uint32_t zp[1024];
+  for (uint32_t i = threadIdx.x; i < 1024; i += 256) zp[i] = (&a.tabs->zpiece[0][0])[i];
+  __syncthreads();
+  const uint64_t b = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (b >= a.count) return;
+  const uint32_t s = a.pstart[b], e = a.pstart[b + 1];
+  if (e - s <= 1 || e > a.max_pieces) return;
+  uint32_t acc = a.partial[s];
+  for (uint32_t g = s + 1; g < e; ++g) {
+    acc = zp[acc & 255u] ^ zp[256 + ((acc >> 8) & 255u)] ^ zp[512 + ((acc >> 16) & 255u)] ^ zp[768 + (acc >> 24)];
+    acc ^= a.partial[g];
+  }
+  emit_block(a, b, ~acc);
+}
+
+__global__ void crc32c_plan_count_kernel(const uint64_t* len, uint64_t count, uint64_t piece_bytes,
+                                         uint32_t* counts) {
+  const uint64_t b = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= count) return;
+  const uint64_t n = len[b];
+  counts[b] = n <= piece_bytes ? 1u : uint32_t((n + piece_bytes - 1) / piece_bytes);
+}
+
+__global__ void crc32c_plan_expand_kernel(const uint32_t* pstart, uint64_t count, uint64_t max_pieces,
+                                          uint32_t* pblk) {
+  const uint64_t b = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= count) return;
+  const uint32_t s = pstart[b], e = pstart[b + 1];
+  for (uint32_t g = s; g < e && g < max_pieces; ++g) pblk[g] = uint32_t(b);
+}
+
+// ------------------------------------------------------------------------------------------------
+// support kernels
+__device__ __forceinline__ uint64_t splitmix_word(uint64_t seed, uint64_t j) {
+  uint64_t z = seed + (j + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Fast path: dst 16-B aligned and stream_offset % 16 == 0; each thread writes 16 B per step.
+__global__ void fill_splitmix_fast_kernel(uint4* dst, uint64_t n16, uint64_t seed, uint64_t w0) {
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n16; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t lo = splitmix_word(seed, w0 + 2 * i), hi = splitmix_word(seed, w0 + 2 * i + 1);
+    dst[i] = make_uint4(uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32));
+  }
+}
+
+__global__ void fill_splitmix_bytes_kernel(uint8_t* dst, uint64_t n, uint64_t seed, uint64_t so) {
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t gpos = so + i;
+    dst[i] = uint8_t(splitmix_word(seed, gpos >> 3) >> (8 * (gpos & 7)));
+  }
+}
+
+__global__ void __launch_bounds__(256) stream_read_kernel(const uint4* src, uint64_t n16, uint32_t* sink) {
+  uint32_t acc = 0;
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const uint4 x0 = src[i], x1 = src[i + stride], x2 = src[i + 2 * stride], x3 = src[i + 3 * stride];
+    acc ^= x0.x ^ x0.y ^ x0.z ^ x0.w ^ x1.x ^ x1.y ^ x1.z ^ x1.w ^ x2.x ^ x2.y ^ x2.z ^ x2.w ^ x3.x ^ x3.y ^ x3.z ^ x3.w;
+  }
+  for (; i < n16; i += stride) {
+    const uint4 x = src[i];
+    acc ^= x.x ^ x.y ^ x.z ^ x.w;
+  }
+  if (acc == 0x9e3779b9u) atomicXor(sink, acc);  // keeps the loads live; practically never stores
+}
+
+}  // namespace kvsep
+
+// ================================================================================================
+// host side
+using namespace kvsep;
+
+struct kvsep_crc32c_ctx {
+  int device = 0;
+  int num_cus = 0;
+  DevTables* d_tabs = nullptr;
+  uint64_t piece_bytes = 256 * 1024;
+  int dynamic = 1;
+  // scratch
+  uint64_t cap_count = 0, cap_pieces = 0;
+  uint32_t* d_counts = nullptr;
+  uint32_t* d_pstart = nullptr;
+  uint32_t* d_pblk = nullptr;
+  uint32_t* d_partial = nullptr;
+  uint32_t* d_counter = nullptr;
+  unsigned long long* d_verify_scratch = nullptr;  // [first_bad, nbad] when the caller passes none
+  void* d_scan_tmp = nullptr;
+  size_t scan_tmp_bytes = 0;
+  // timing
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
+  std::vector<hipEvent_t> ev_pool;
+  // host form
+  HostStaging staging;
+  std::mutex mu;
+};
+
+namespace {
+thread_local std::string g_last_error;
+
+int set_err(int code, const char* what, hipError_t e = hipSuccess) {
+  char buf[512];
+  if (e != hipSuccess)
+    snprintf(buf, sizeof buf, "%s: %s (%d)", what, hipGetErrorString(e), int(e));
+  else
+    snprintf(buf, sizeof buf, "%s", what);
+  g_last_error = buf;
+  return code;
+}
+
+#define KVSEP_HIP(call)                                              \
+  do {                                                               \
+    hipError_t _e = (call);                                          \
+    if (_e != hipSuccess) return set_err(KVSEP_EHIP, #call, _e);     \
+  } while (0)
+
+int upload_tables(kvsep_crc32c_ctx* c) {
+  DevTables h;
+  gf2::byte_tables(gf2::zero_bytes_map(1024), &h.z1024[0][0]);
+  gf2::byte_tables(gf2::zero_bytes_map(4), &h.z4[0][0]);
+  for (int j = 0; j < 6; ++j) gf2::byte_tables(gf2::zero_bytes_map(16ull << j), &h.ztree[j][0][0]);
+  for (uint32_t b = 0; b < 256; ++b) h.byte1[b] = gf2::byte_table_entry(b);
+  gf2::byte_tables(gf2::zero_bytes_map(c->piece_bytes), &h.zpiece[0][0]);
+  if (!c->d_tabs) KVSEP_HIP(hipMalloc(&c->d_tabs, sizeof(DevTables)));
+  KVSEP_HIP(hipMemcpy(c->d_tabs, &h, sizeof(DevTables), hipMemcpyHostToDevice));
+  return KVSEP_OK;
+}
+
+void free_scratch(kvsep_crc32c_ctx* c) {
+  hipFree(c->d_counts); hipFree(c->d_pstart); hipFree(c->d_pblk); hipFree(c->d_partial);
+  hipFree(c->d_scan_tmp);
+  c->d_counts = c->d_pstart = c->d_pblk = c->d_partial = nullptr;
+  c->d_scan_tmp = nullptr;
+  c->cap_count = c->cap_pieces = 0;
+  c->scan_tmp_bytes = 0;
+}
+
+int ensure_scratch(kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes) {
+  const uint64_t pieces = count + total_bytes / c->piece_bytes + 1;
+  if (count > 0xffffffffull || pieces > 0xffffffffull) return set_err(KVSEP_EINVAL, "batch too large for u32 piece indices");
+  if (count <= c->cap_count && pieces <= c->cap_pieces) return KVSEP_OK;
+  const uint64_t nc = std::max<uint64_t>(count, c->cap_count), np = std::max<uint64_t>(pieces, c->cap_pieces);
+  KVSEP_HIP(hipDeviceSynchronize());
+  free_scratch(c);
+  KVSEP_HIP(hipMalloc(&c->d_counts, nc * 4));
+  KVSEP_HIP(hipMalloc(&c->d_pstart, (nc + 1) * 4));
+  KVSEP_HIP(hipMalloc(&c->d_pblk, np * 4));
+  KVSEP_HIP(hipMalloc(&c->d_partial, np * 4));
+  size_t tb = 0;
+  KVSEP_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, c->d_counts, c->d_pstart + 1, int(nc), hipStream_t(0)));
+  KVSEP_HIP(hipMalloc(&c->d_scan_tmp, tb));
+  c->scan_tmp_bytes = tb;
+  c->cap_count = nc;
+  c->cap_pieces = np;
+  return KVSEP_OK;
+}
+
+hipEvent_t take_event(kvsep_crc32c_ctx* c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+int launch_batch(kvsep_crc32c_ctx* c, hipStream_t s, const void* base, const uint64_t* off, const uint64_t* len,
+                 const uint32_t* init, const uint32_t* expect, uint32_t* out, uint64_t* first_bad, uint64_t* nbad,
+                 uint64_t count, uint64_t total_bytes, uint64_t max_len) {
+  if (!base || !off || !len || !out) return set_err(KVSEP_EINVAL, "null pointer argument");
+  KVSEP_HIP(hipSetDevice(c->device));
+  const bool planned = !(max_len != 0 && max_len <= c->piece_bytes);
+  PiecesArgs a{};
+  a.base = static_cast<const uint8_t*>(base);
+  a.off = off;
+  a.len = len;
+  a.init = init;
+  a.out = out;
+  a.expect = expect;
+  a.count = count;
+  a.piece_bytes = c->piece_bytes;
+  a.tabs = c->d_tabs;
+  if (expect) {
+    if (!first_bad || !nbad) {
+      if (!c->d_verify_scratch) KVSEP_HIP(hipMalloc(&c->d_verify_scratch, 16));
+      first_bad = reinterpret_cast<uint64_t*>(c->d_verify_scratch);
+      nbad = reinterpret_cast<uint64_t*>(c->d_verify_scratch + 1);
+    }
+    a.first_bad = reinterpret_cast<unsigned long long*>(first_bad);
+    a.nbad = reinterpret_cast<unsigned long long*>(nbad);
+    KVSEP_HIP(hipMemsetAsync(first_bad, 0xff, 8, s));
+    KVSEP_HIP(hipMemsetAsync(nbad, 0, 8, s));
+  }
+  if (count == 0) return KVSEP_OK;
+  if (planned) {
+    int rc = ensure_scratch(c, count, total_bytes);
+    if (rc) return rc;
+    a.pstart = c->d_pstart;
+    a.pblk = c->d_pblk;
+    a.partial = c->d_partial;
+    a.max_pieces = c->cap_pieces;
+    const unsigned nb = unsigned((count + 255) / 256);
+    crc32c_plan_count_kernel<<<nb, 256, 0, s>>>(len, count, c->piece_bytes, c->d_counts);
+    KVSEP_HIP(hipGetLastError());
+    KVSEP_HIP(hipMemsetAsync(c->d_pstart, 0, 4, s));
+    size_t tb = c->scan_tmp_bytes;
+    KVSEP_HIP(hipcub::DeviceScan::InclusiveSum(c->d_scan_tmp, tb, c->d_counts, c->d_pstart + 1, int(count), s));
+    crc32c_plan_expand_kernel<<<nb, 256, 0, s>>>(c->d_pstart, count, c->cap_pieces, c->d_pblk);
+    KVSEP_HIP(hipGetLastError());
+  } else {
+    a.max_pieces = count;
+  }
+  if (c->dynamic) {
+    if (!c->d_counter) KVSEP_HIP(hipMalloc(&c->d_counter, 16));
+    a.work_counter = c->d_counter;
+    KVSEP_HIP(hipMemsetAsync(c->d_counter, 0, 4, s));
+  }
+  const unsigned grid = unsigned(c->num_cus);  // one 16-wave workgroup per CU, persistent
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c->timing) {
+    e0 = take_event(c);
+    e1 = take_event(c);
+    if (e0 && e1) KVSEP_HIP(hipEventRecord(e0, s));
+  }
+  if (planned) {
+    if (c->dynamic) crc32c_pieces_kernel<true, true><<<grid, kWgThreads, 0, s>>>(a);
+    else crc32c_pieces_kernel<true, false><<<grid, kWgThreads, 0, s>>>(a);
+  } else {
+    if (c->dynamic) crc32c_pieces_kernel<false, true><<<grid, kWgThreads, 0, s>>>(a);
+    else crc32c_pieces_kernel<false, false><<<grid, kWgThreads, 0, s>>>(a);
+  }
+  KVSEP_HIP(hipGetLastError());
+  if (c->timing && e0 && e1) {
+    KVSEP_HIP(hipEventRecord(e1, s));
+    c->ev_pending.emplace_back(e0, e1);
+  }
+  if (planned) {
+    crc32c_combine_kernel<<<unsigned((count + 255) / 256), 256, 0, s>>>(a);
+    KVSEP_HIP(hipGetLastError());
+  }
+  return KVSEP_OK;
+}
+}  // namespace
+
+namespace kvsep {
+int device_batch_locked(kvsep_crc32c_ctx* c, hipStream_t s, const void* base, const uint64_t* off,
+                        const uint64_t* len, const uint32_t* init, uint32_t* out, uint64_t count,
+                        uint64_t total_bytes, uint64_t max_len) {
+  return launch_batch(c, s, base, off, len, init, nullptr, out, nullptr, nullptr, count, total_bytes, max_len);
+}
+HostStaging& ctx_staging(kvsep_crc32c_ctx* c) { return c->staging; }
+std::mutex& ctx_mutex(kvsep_crc32c_ctx* c) { return c->mu; }
+int ctx_device(kvsep_crc32c_ctx* c) { return c->device; }
+uint64_t ctx_piece_bytes(kvsep_crc32c_ctx* c) { return c->piece_bytes; }
+void set_last_error(const char* msg) { g_last_error = msg; }
+}  // namespace kvsep
+
+extern "C" {
+
+int kvsep_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int kvsep_crc32c_ctx_create(int device, kvsep_crc32c_ctx** out) {
+  if (!out) return set_err(KVSEP_EINVAL, "out is null");
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0)
+    return set_err(KVSEP_ENODEV, "no HIP device with that ordinal");
+  hipDeviceProp_t prop;
+  KVSEP_HIP(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    std::string m = std::string("device is ") + prop.gcnArchName + ", this build targets gfx950 only";
+    return set_err(KVSEP_ENODEV, m.c_str());
+  }
+  auto* c = new kvsep_crc32c_ctx();
+  c->device = device;
+  c->num_cus = prop.multiProcessorCount;
+  KVSEP_HIP(hipSetDevice(device));
+  int rc = upload_tables(c);
+  if (rc) {
+    delete c;
+    return rc;
+  }
+  *out = c;
+  return KVSEP_OK;
+}
+
+void kvsep_crc32c_ctx_destroy(kvsep_crc32c_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipDeviceSynchronize();
+  free_scratch(c);
+  hipFree(c->d_tabs);
+  hipFree(c->d_counter);
+  hipFree(c->d_verify_scratch);
+  for (auto& p : c->ev_pending) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
+  for (auto e : c->ev_pool) hipEventDestroy(e);
+  release_staging(c->staging);
+  delete c;
+}
+
+int kvsep_crc32c_ctx_set_piece_bytes(kvsep_crc32c_ctx* c, uint64_t piece_bytes) {
+  if (!c || piece_bytes < 1024 || piece_bytes % 1024) return set_err(KVSEP_EINVAL, "piece_bytes must be a multiple of 1 KiB");
+  std::lock_guard<std::mutex> g(c->mu);
+  KVSEP_HIP(hipSetDevice(c->device));
+  KVSEP_HIP(hipDeviceSynchronize());
+  c->piece_bytes = piece_bytes;
+  free_scratch(c);
+  return upload_tables(c);
+}
+
+int kvsep_crc32c_ctx_set_schedule(kvsep_crc32c_ctx* c, int dynamic) {
+  if (!c) return set_err(KVSEP_EINVAL, "null ctx");
+  c->dynamic = dynamic ? 1 : 0;
+  return KVSEP_OK;
+}
+
+int kvsep_crc32c_reserve(kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes) {
+  if (!c) return set_err(KVSEP_EINVAL, "null ctx");
+  std::lock_guard<std::mutex> g(c->mu);
+  KVSEP_HIP(hipSetDevice(c->device));
+  return ensure_scratch(c, count, total_bytes);
+}
+
+int kvsep_crc32c_ctx_set_timing(kvsep_crc32c_ctx* c, int enable) {
+  if (!c) return set_err(KVSEP_EINVAL, "null ctx");
+  c->timing = enable != 0;
+  return KVSEP_OK;
+}
+
+int kvsep_crc32c_ctx_get_timing(kvsep_crc32c_ctx* c, double* total_ms, uint64_t* launches) {
+  if (!c) return set_err(KVSEP_EINVAL, "null ctx");
+  std::lock_guard<std::mutex> g(c->mu);
+  double ms = 0;
+  uint64_t n = 0;
+  for (auto& p : c->ev_pending) {
+    KVSEP_HIP(hipEventSynchronize(p.second));
+    float t = 0;
+    KVSEP_HIP(hipEventElapsedTime(&t, p.first, p.second));
+    ms += t;
+    ++n;
+    c->ev_pool.push_back(p.first);
+    c->ev_pool.push_back(p.second);
+  }
+  c->ev_pending.clear();
+  if (total_ms) *total_ms = ms;
+  if (launches) *launches = n;
+  return KVSEP_OK;
+}
+
+int kvsep_crc32c_batch_device(kvsep_crc32c_ctx* c, void* stream, const void* base, const uint64_t* off,
+                              const uint64_t* len, const uint32_t* init, uint32_t* out, uint64_t count,
+                              uint64_t total_bytes, uint64_t max_len) {
+  if (!c) return set_err(KVSEP_EINVAL, "null ctx");
+  std::lock_guard<std::mutex> g(c->mu);
+  return launch_batch(c, static_cast<hipStream_t>(stream), base, off, len, init, nullptr, out, nullptr, nullptr,
+                      count, total_bytes, max_len);
+}
+
+int kvsep_crc32c_verify_device(kvsep_crc32c_ctx* c, void* stream, const void* base, const uint64_t* off,
+                               const uint64_t* len, const uint32_t* init, const uint32_t* expected_masked,
+                               uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count,
+                               uint64_t total_bytes, uint64_t max_len) {
+  if (!c || !expected_masked) return set_err(KVSEP_EINVAL, "null ctx or expected_masked");
+  std::lock_guard<std::mutex> g(c->mu);
+  return launch_batch(c, static_cast<hipStream_t>(stream), base, off, len, init, expected_masked, out, first_bad,
+                      nbad, count, total_bytes, max_len);
+}
+
+int kvsep_fill_splitmix64_device(void* stream, void* dst, uint64_t nbytes, uint64_t seed, uint64_t stream_offset) {
+  if (!dst && nbytes) return set_err(KVSEP_EINVAL, "null dst");
+  if (!nbytes) return KVSEP_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const unsigned grid = 256 * 8;
+  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0 && (stream_offset & 15) == 0) {
+    const uint64_t n16 = nbytes / 16;
+    if (n16) fill_splitmix_fast_kernel<<<grid, 256, 0, s>>>(static_cast<uint4*>(dst), n16, seed, stream_offset / 8);
+    const uint64_t rest = nbytes - n16 * 16;
+    if (rest)
+      fill_splitmix_bytes_kernel<<<1, 64, 0, s>>>(static_cast<uint8_t*>(dst) + n16 * 16, rest, seed,
+                                                  stream_offset + n16 * 16);
+  } else {
+    fill_splitmix_bytes_kernel<<<grid, 256, 0, s>>>(static_cast<uint8_t*>(dst), nbytes, seed, stream_offset);
+  }
+  KVSEP_HIP(hipGetLastError());
+  return KVSEP_OK;
+}
+
+int kvsep_stream_read_device(kvsep_crc32c_ctx* c, void* stream, const void* src, uint64_t nbytes, uint32_t* sink) {
+  if (!c || !src || !sink) return set_err(KVSEP_EINVAL, "null argument");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint64_t n16 = nbytes / 16;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->timing) {
+    e0 = take_event(c);
+    e1 = take_event(c);
+    if (e0 && e1) KVSEP_HIP(hipEventRecord(e0, s));
+  }
+  stream_read_kernel<<<unsigned(c->num_cus) * 8, 256, 0, s>>>(static_cast<const uint4*>(src), n16, sink);
+  KVSEP_HIP(hipGetLastError());
+  if (c->timing && e0 && e1) {
+    KVSEP_HIP(hipEventRecord(e1, s));
+    c->ev_pending.emplace_back(e0, e1);
+  }
+  return KVSEP_OK;
+}
+
+const char* kvsep_last_error(void) { return g_last_error.c_str(); }
+
+}  // extern "C"

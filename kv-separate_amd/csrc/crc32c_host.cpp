@@ -1,0 +1,410 @@
+// crc32c_host.cpp -- host half of libkvsep_crc32c: the scalar drop-in (Extend / Value / Mask /
+// Unmask / AcceleratedCRC32C), the host-memory batch entry points (pinned staging, H2D, kernel,
+// D2H over two streams), and build info.
+//
+// Reference interfaces replaced (see include/kvsep_crc32c.h for the full list):
+//   util/crc32c.h:17   leveldb::crc32c::Extend      -> kvsep_crc32c_extend
+//   port/port_stdcxx.h:142 port::AcceleratedCRC32C  -> kvsep_accelerated_crc32c
+#include <hip/hip_runtime.h>
+#include <nmmintrin.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/kvsep_crc32c.h"
+#include "kvsep_internal.h"
+
+namespace kvsep {
+
+void release_staging(HostStaging& s) {
+  for (int i = 0; i < HostStaging::kSlots; ++i) {
+    if (s.stream[i]) hipStreamSynchronize(s.stream[i]);
+    hipHostFree(s.h_data[i]); hipHostFree(s.h_desc[i]); hipHostFree(s.h_init[i]); hipHostFree(s.h_out[i]);
+    hipFree(s.d_data[i]); hipFree(s.d_desc[i]); hipFree(s.d_init[i]); hipFree(s.d_out[i]);
+    if (s.done[i]) hipEventDestroy(s.done[i]);
+    if (s.stream[i]) hipStreamDestroy(s.stream[i]);
+  }
+  s = HostStaging();
+}
+
+namespace {
+
+std::atomic<uint64_t> g_offload_threshold{64ull << 20};
+
+// ------------------------------------------------------------------ host CRC (SSE4.2)
+// The crc32 instruction implements exactly the reflected Castagnoli register update of
+// util/crc32c.cc:287-292 without the ~0 conditioning, so Extend = ~crc32(~init, data).
+// Three independent streams hide the instruction's 3-cycle latency; they are merged with
+// the zero-byte shift R(A||B) = Z_|B|(R(A)) ^ R(B), Z evaluated with the crc32 instruction itself
+// on a 32-bit value followed by zeros is avoided by using precomputed shift tables.
+struct ShiftTables {
+  uint32_t t[4][256];
+};
+
+uint32_t sw_byte(uint32_t b) {
+  uint32_t r = b;
+  for (int k = 0; k < 8; ++k) r = (r >> 1) ^ (0x82F63B78u & (0u - (r & 1u)));
+  return r;
+}
+
+uint32_t zero_shift_slow(uint32_t reg, uint64_t nbytes) {
+  for (uint64_t i = 0; i < nbytes; ++i) reg = sw_byte(reg & 0xffu) ^ (reg >> 8);
+  return reg;
+}
+
+constexpr uint64_t kLaneBlock = 4096;  // bytes per stream per round of the 3-way loop
+const ShiftTables& shift_tables() {
+  static const ShiftTables tabs = [] {
+    ShiftTables s;
+    for (int k = 0; k < 4; ++k)
+      for (uint32_t b = 0; b < 256; ++b) s.t[k][b] = zero_shift_slow(b << (8 * k), kLaneBlock);
+    return s;
+  }();
+  return tabs;
+}
+
+inline uint32_t shift_lane(const ShiftTables& s, uint32_t v) {
+  return s.t[0][v & 0xffu] ^ s.t[1][(v >> 8) & 0xffu] ^ s.t[2][(v >> 16) & 0xffu] ^ s.t[3][v >> 24];
+}
+
+__attribute__((target("sse4.2"))) uint32_t host_crc(uint32_t init, const uint8_t* p, size_t n) {
+  uint64_t l = uint32_t(~init);
+  while (n && (reinterpret_cast<uintptr_t>(p) & 7)) {
+    l = _mm_crc32_u8(uint32_t(l), *p++);
+    --n;
+  }
+  if (n >= 3 * kLaneBlock) {
+    const ShiftTables& st = shift_tables();
+    while (n >= 3 * kLaneBlock) {
+      uint64_t a = l, b = 0, c = 0;
+      const uint8_t* pa = p;
+      const uint8_t* pb = p + kLaneBlock;
+      const uint8_t* pc = p + 2 * kLaneBlock;
+      for (uint64_t i = 0; i < kLaneBlock; i += 8) {
+        uint64_t wa, wb, wc;
+        std::memcpy(&wa, pa + i, 8);
+        std::memcpy(&wb, pb + i, 8);
+        std::memcpy(&wc, pc + i, 8);
+        a = _mm_crc32_u64(a, wa);
+        b = _mm_crc32_u64(b, wb);
+        c = _mm_crc32_u64(c, wc);
+      }
+      // R(A||B||C) = Z(Z(a) ^ b) ^ c with Z = advance over kLaneBlock zero bytes
+      l = shift_lane(st, shift_lane(st, uint32_t(a)) ^ uint32_t(b)) ^ uint32_t(c);
+      p += 3 * kLaneBlock;
+      n -= 3 * kLaneBlock;
+    }
+  }
+  while (n >= 8) {
+    uint64_t w;
+    std::memcpy(&w, p, 8);
+    l = _mm_crc32_u64(l, w);
+    p += 8;
+    n -= 8;
+  }
+  while (n) {
+    l = _mm_crc32_u8(uint32_t(l), *p++);
+    --n;
+  }
+  return ~uint32_t(l);
+}
+
+// ------------------------------------------------------------------ staging pipeline
+constexpr uint64_t kSlotBytes = 64ull << 20;
+constexpr uint64_t kSlotBlocks = 1ull << 16;
+
+int hip_fail(const char* what, hipError_t e) {
+  char buf[384];
+  snprintf(buf, sizeof buf, "%s: %s (%d)", what, hipGetErrorString(e), int(e));
+  set_last_error(buf);
+  return KVSEP_EHIP;
+}
+
+#define KVSEP_HIPH(call)                              \
+  do {                                                \
+    hipError_t _e = (call);                           \
+    if (_e != hipSuccess) return hip_fail(#call, _e); \
+  } while (0)
+
+int ensure_staging(kvsep_crc32c_ctx* c) {
+  HostStaging& s = ctx_staging(c);
+  if (s.ready) return KVSEP_OK;
+  KVSEP_HIPH(hipSetDevice(ctx_device(c)));
+  s.bytes = kSlotBytes;
+  s.max_blocks = kSlotBlocks;
+  for (int i = 0; i < HostStaging::kSlots; ++i) {
+    KVSEP_HIPH(hipHostMalloc(reinterpret_cast<void**>(&s.h_data[i]), s.bytes, hipHostMallocDefault));
+    KVSEP_HIPH(hipHostMalloc(reinterpret_cast<void**>(&s.h_desc[i]), 2 * s.max_blocks * 8, hipHostMallocDefault));
+    KVSEP_HIPH(hipHostMalloc(reinterpret_cast<void**>(&s.h_init[i]), s.max_blocks * 4, hipHostMallocDefault));
+    KVSEP_HIPH(hipHostMalloc(reinterpret_cast<void**>(&s.h_out[i]), s.max_blocks * 4, hipHostMallocDefault));
+    KVSEP_HIPH(hipMalloc(&s.d_data[i], s.bytes));
+    KVSEP_HIPH(hipMalloc(&s.d_desc[i], 2 * s.max_blocks * 8));
+    KVSEP_HIPH(hipMalloc(&s.d_init[i], s.max_blocks * 4));
+    KVSEP_HIPH(hipMalloc(&s.d_out[i], s.max_blocks * 4));
+    KVSEP_HIPH(hipStreamCreateWithFlags(&s.stream[i], hipStreamNonBlocking));
+    KVSEP_HIPH(hipEventCreateWithFlags(&s.done[i], hipEventDisableTiming));
+  }
+  s.ready = true;
+  return KVSEP_OK;
+}
+
+bool is_pinned(const void* p) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return attr.type == hipMemoryTypeHost;
+}
+
+// A submitted slot: which caller indices its h_out entries belong to.
+struct SlotJob {
+  bool busy = false;
+  uint64_t first = 0, n = 0;  // caller indices [first, first+n) in order
+};
+
+// Collect results of a slot into the caller's out[], once its D2H has landed.
+int retire(HostStaging& s, int slot, SlotJob& job, uint32_t* out) {
+  if (!job.busy) return KVSEP_OK;
+  KVSEP_HIPH(hipEventSynchronize(s.done[slot]));
+  std::memcpy(out + job.first, s.h_out[slot], job.n * 4);
+  job.busy = false;
+  return KVSEP_OK;
+}
+
+// Submit the staged group in `slot`: the payload already sits in d_data (H2D queued) or h_data.
+int submit(kvsep_crc32c_ctx* c, HostStaging& s, int slot, uint64_t nblk, uint64_t payload, uint64_t max_len,
+           const uint8_t* pinned_src, bool have_init) {
+  hipStream_t st = s.stream[slot];
+  const uint8_t* src = pinned_src ? pinned_src : s.h_data[slot];
+  KVSEP_HIPH(hipMemcpyAsync(s.d_data[slot], src, payload, hipMemcpyHostToDevice, st));
+  KVSEP_HIPH(hipMemcpyAsync(s.d_desc[slot], s.h_desc[slot], nblk * 8, hipMemcpyHostToDevice, st));
+  KVSEP_HIPH(hipMemcpyAsync(s.d_desc[slot] + s.max_blocks, s.h_desc[slot] + s.max_blocks, nblk * 8,
+                            hipMemcpyHostToDevice, st));
+  if (have_init) KVSEP_HIPH(hipMemcpyAsync(s.d_init[slot], s.h_init[slot], nblk * 4, hipMemcpyHostToDevice, st));
+  int rc = device_batch_locked(c, st, s.d_data[slot], s.d_desc[slot], s.d_desc[slot] + s.max_blocks,
+                               have_init ? s.d_init[slot] : nullptr, s.d_out[slot], nblk, payload, max_len);
+  if (rc) return rc;
+  KVSEP_HIPH(hipMemcpyAsync(s.h_out[slot], s.d_out[slot], nblk * 4, hipMemcpyDeviceToHost, st));
+  KVSEP_HIPH(hipEventRecord(s.done[slot], st));
+  return KVSEP_OK;
+}
+
+// One block longer than a slot: chain slot-sized segments, each seeded with the previous CRC.
+int big_block(kvsep_crc32c_ctx* c, HostStaging& s, SlotJob* jobs, uint32_t* out, const uint8_t* p, uint64_t n,
+              uint32_t init, bool pinned, uint32_t* result) {
+  for (int i = 0; i < HostStaging::kSlots; ++i) {
+    int rc = retire(s, i, jobs[i], out);
+    if (rc) return rc;
+  }
+  uint32_t crc = init;
+  int slot = 0;
+  // Segments run on one stream; host data of segment k+1 is staged while segment k computes.
+  for (uint64_t done = 0; done < n; done += s.bytes, slot ^= 1) {
+    const uint64_t seg = std::min<uint64_t>(s.bytes, n - done);
+    KVSEP_HIPH(hipEventSynchronize(s.done[slot]));  // previous use of this slot's buffers finished
+    if (!pinned) std::memcpy(s.h_data[slot], p + done, seg);
+    s.h_desc[slot][0] = 0;
+    s.h_desc[slot][s.max_blocks] = seg;
+    hipStream_t st = s.stream[0];
+    KVSEP_HIPH(hipMemcpyAsync(s.d_data[slot], pinned ? p + done : s.h_data[slot], seg, hipMemcpyHostToDevice, st));
+    KVSEP_HIPH(hipMemcpyAsync(s.d_desc[slot], s.h_desc[slot], 8, hipMemcpyHostToDevice, st));
+    KVSEP_HIPH(hipMemcpyAsync(s.d_desc[slot] + s.max_blocks, s.h_desc[slot] + s.max_blocks, 8, hipMemcpyHostToDevice, st));
+    if (done == 0) {
+      s.h_init[slot][0] = crc;
+      KVSEP_HIPH(hipMemcpyAsync(s.d_init[slot], s.h_init[slot], 4, hipMemcpyHostToDevice, st));
+    } else {  // seed with the previous segment's CRC, straight from device memory
+      KVSEP_HIPH(hipMemcpyAsync(s.d_init[slot], s.d_out[slot ^ 1], 4, hipMemcpyDeviceToDevice, st));
+    }
+    int rc = device_batch_locked(c, st, s.d_data[slot], s.d_desc[slot], s.d_desc[slot] + s.max_blocks,
+                                 s.d_init[slot], s.d_out[slot], 1, seg, seg);
+    if (rc) return rc;
+    KVSEP_HIPH(hipEventRecord(s.done[slot], st));
+  }
+  slot ^= 1;  // slot of the last segment
+  KVSEP_HIPH(hipMemcpyAsync(s.h_out[slot], s.d_out[slot], 4, hipMemcpyDeviceToHost, s.stream[0]));
+  KVSEP_HIPH(hipStreamSynchronize(s.stream[0]));
+  *result = s.h_out[slot][0];
+  return KVSEP_OK;
+}
+
+kvsep_crc32c_ctx* default_ctx() {
+  static std::once_flag once;
+  static kvsep_crc32c_ctx* ctx = nullptr;
+  std::call_once(once, [] {
+    if (kvsep_crc32c_ctx_create(0, &ctx) != KVSEP_OK) {
+      std::fprintf(stderr, "kvsep_crc32c: GPU offload unavailable: %s\n", kvsep_last_error());
+      ctx = nullptr;
+    }
+  });
+  return ctx;
+}
+
+}  // namespace
+}  // namespace kvsep
+
+using namespace kvsep;
+
+extern "C" {
+
+uint32_t kvsep_crc32c_extend_host(uint32_t init_crc, const char* data, size_t n) {
+  return host_crc(init_crc, reinterpret_cast<const uint8_t*>(data), n);
+}
+
+uint32_t kvsep_crc32c_extend(uint32_t init_crc, const char* data, size_t n) {
+  if (n >= g_offload_threshold.load(std::memory_order_relaxed)) {
+    kvsep_crc32c_ctx* c = default_ctx();
+    if (c) {
+      const uint64_t off = 0, len = n;
+      uint32_t out = 0;
+      if (kvsep_crc32c_batch_host_span(c, data, n, &off, &len, &init_crc, &out, 1) == KVSEP_OK) return out;
+      std::fprintf(stderr, "kvsep_crc32c: GPU offload failed: %s\n", kvsep_last_error());
+    }
+    // Extend is total (util/crc32c.h:17 has no error channel): a strict deployment aborts instead.
+    if (std::getenv("KVSEP_STRICT_GPU")) std::abort();
+  }
+  return host_crc(init_crc, reinterpret_cast<const uint8_t*>(data), n);
+}
+
+uint32_t kvsep_crc32c_value(const char* data, size_t n) { return kvsep_crc32c_extend(0, data, n); }
+
+uint32_t kvsep_crc32c_mask(uint32_t crc) { return ((crc >> 15) | (crc << 17)) + 0xa282ead8u; }
+
+uint32_t kvsep_crc32c_unmask(uint32_t masked_crc) {
+  const uint32_t rot = masked_crc - 0xa282ead8u;
+  return (rot >> 17) | (rot << 15);
+}
+
+uint32_t kvsep_accelerated_crc32c(uint32_t crc, const char* buf, size_t size) {
+  return kvsep_crc32c_extend(crc, buf, size);
+}
+
+void kvsep_set_offload_threshold(uint64_t nbytes) { g_offload_threshold.store(nbytes); }
+
+int kvsep_crc32c_batch_host_span(kvsep_crc32c_ctx* c, const char* host_base, uint64_t span_bytes,
+                                 const uint64_t* off, const uint64_t* len, const uint32_t* init, uint32_t* out,
+                                 uint64_t count) {
+  if (!c || (!host_base && span_bytes) || (count && (!off || !len || !out))) {
+    set_last_error("null argument");
+    return KVSEP_EINVAL;
+  }
+  for (uint64_t i = 0; i < count; ++i)
+    if (off[i] > span_bytes || len[i] > span_bytes - off[i]) {
+      set_last_error("block outside span");
+      return KVSEP_EINVAL;
+    }
+  std::lock_guard<std::mutex> g(ctx_mutex(c));
+  int rc = ensure_staging(c);
+  if (rc) return rc;
+  HostStaging& s = ctx_staging(c);
+  const uint8_t* base = reinterpret_cast<const uint8_t*>(host_base);
+  const bool pinned = span_bytes && is_pinned(host_base);
+  SlotJob jobs[HostStaging::kSlots];
+  int slot = 0;
+  uint64_t i = 0;
+  while (i < count) {
+    if (len[i] > s.bytes) {  // long block: chained segments
+      uint32_t r = 0;
+      rc = big_block(c, s, jobs, out, base + off[i], len[i], init ? init[i] : 0u, pinned, &r);
+      if (rc) return rc;
+      out[i] = r;
+      ++i;
+      continue;
+    }
+    // group consecutive blocks whose covering range fits one slot
+    uint64_t lo = off[i], hi = off[i] + len[i], j = i + 1, max_len = len[i];
+    while (j < count && j - i < s.max_blocks && len[j] <= s.bytes) {
+      const uint64_t nlo = std::min(lo, off[j]), nhi = std::max(hi, off[j] + len[j]);
+      if (nhi - nlo > s.bytes) break;
+      lo = nlo; hi = nhi; max_len = std::max(max_len, len[j]);
+      ++j;
+    }
+    rc = retire(s, slot, jobs[slot], out);
+    if (rc) return rc;
+    const uint64_t nblk = j - i;
+    for (uint64_t k = 0; k < nblk; ++k) {
+      s.h_desc[slot][k] = off[i + k] - lo;
+      s.h_desc[slot][s.max_blocks + k] = len[i + k];
+      if (init) s.h_init[slot][k] = init[i + k];
+    }
+    if (!pinned) std::memcpy(s.h_data[slot], base + lo, hi - lo);
+    rc = submit(c, s, slot, nblk, hi - lo, max_len, pinned ? base + lo : nullptr, init != nullptr);
+    if (rc) return rc;
+    jobs[slot].busy = true;
+    jobs[slot].first = i;
+    jobs[slot].n = nblk;
+    slot ^= 1;
+    i = j;
+  }
+  for (int k = 0; k < HostStaging::kSlots; ++k) {
+    rc = retire(s, k, jobs[k], out);
+    if (rc) return rc;
+  }
+  return KVSEP_OK;
+}
+
+int kvsep_crc32c_batch_host(kvsep_crc32c_ctx* c, const uint32_t* init, const char* const* ptr, const uint64_t* len,
+                            uint32_t* out, uint64_t count) {
+  if (!c || (count && (!ptr || !len || !out))) {
+    set_last_error("null argument");
+    return KVSEP_EINVAL;
+  }
+  std::lock_guard<std::mutex> g(ctx_mutex(c));
+  int rc = ensure_staging(c);
+  if (rc) return rc;
+  HostStaging& s = ctx_staging(c);
+  SlotJob jobs[HostStaging::kSlots];
+  int slot = 0;
+  uint64_t i = 0;
+  while (i < count) {
+    if (len[i] > s.bytes) {
+      uint32_t r = 0;
+      rc = big_block(c, s, jobs, out, reinterpret_cast<const uint8_t*>(ptr[i]), len[i], init ? init[i] : 0u,
+                     is_pinned(ptr[i]), &r);
+      if (rc) return rc;
+      out[i] = r;
+      ++i;
+      continue;
+    }
+    rc = retire(s, slot, jobs[slot], out);
+    if (rc) return rc;
+    uint64_t used = 0, j = i, max_len = 0;
+    // gather: blocks packed back to back, each at a 16-B aligned staging offset
+    while (j < count && j - i < s.max_blocks && len[j] <= s.bytes) {
+      const uint64_t at = (used + 15) & ~uint64_t(15);
+      if (at + len[j] > s.bytes) break;
+      if (len[j]) std::memcpy(s.h_data[slot] + at, ptr[j], len[j]);
+      s.h_desc[slot][j - i] = at;
+      s.h_desc[slot][s.max_blocks + (j - i)] = len[j];
+      if (init) s.h_init[slot][j - i] = init[j];
+      max_len = std::max(max_len, len[j]);
+      used = at + len[j];
+      ++j;
+    }
+    rc = submit(c, s, slot, j - i, used, max_len, nullptr, init != nullptr);
+    if (rc) return rc;
+    jobs[slot].busy = true;
+    jobs[slot].first = i;
+    jobs[slot].n = j - i;
+    slot ^= 1;
+    i = j;
+  }
+  for (int k = 0; k < HostStaging::kSlots; ++k) {
+    rc = retire(s, k, jobs[k], out);
+    if (rc) return rc;
+  }
+  return KVSEP_OK;
+}
+
+const char* kvsep_build_info(void) {
+  return "kvsep_crc32c: gfx950 HIP kernels (LDS-replicated Z_1024 stride chains, v_perm addressing), "
+         "host SSE4.2 path, ABI 1";
+}
+
+}  // extern "C"

@@ -1,0 +1,295 @@
+"""kvsep -- Python binding (ctypes) of libkvsep_crc32c.so for tests and bench.
+
+The product is the C ABI in include/kvsep_crc32c.h (C++ host code + gfx950 HIP kernels); this module
+only marshals arguments.  It mirrors the reference's util/crc32c.h interface (extend / value / mask /
+unmask, util/crc32c.h:17-38) and adds the batched device/host entry points.
+
+There is no CPU fallback here: if the shared library is missing, importing the GPU entry points
+raises; if no gfx950 device is present, Context() raises.  The oracle under oracle/ is never used.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import sys
+
+try:  # torch first: its libamdhip64.so.7 then serves our library too (same soname, one HIP runtime)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the host-only entry points
+    torch = None
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkvsep_crc32c.so")
+HEADER_PATH = os.path.join(_HERE, "..", "..", "include", "kvsep_crc32c.h")
+
+KVSEP_OK = 0
+MASK_DELTA = 0xA282EAD8  # util/crc32c.h:22
+
+_lib = None
+
+
+class KvsepError(RuntimeError):
+    pass
+
+
+def _u32p():
+    return ctypes.POINTER(ctypes.c_uint32)
+
+
+def _u64p():
+    return ctypes.POINTER(ctypes.c_uint64)
+
+
+_SIGS = {
+    "kvsep_crc32c_extend": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
+    "kvsep_crc32c_value": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_size_t]),
+    "kvsep_crc32c_mask": (ctypes.c_uint32, [ctypes.c_uint32]),
+    "kvsep_crc32c_unmask": (ctypes.c_uint32, [ctypes.c_uint32]),
+    "kvsep_accelerated_crc32c": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
+    "kvsep_set_offload_threshold": (None, [ctypes.c_uint64]),
+    "kvsep_crc32c_extend_host": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
+    "kvsep_crc32c_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "kvsep_crc32c_ctx_destroy": (None, [ctypes.c_void_p]),
+    "kvsep_crc32c_ctx_set_piece_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
+    "kvsep_crc32c_ctx_set_schedule": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "kvsep_crc32c_reserve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]),
+    "kvsep_crc32c_ctx_set_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "kvsep_crc32c_ctx_get_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                                   ctypes.POINTER(ctypes.c_uint64)]),
+    "kvsep_crc32c_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                 ctypes.c_uint64, ctypes.c_uint64]),
+    "kvsep_crc32c_verify_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                                  ctypes.c_uint64]),
+    "kvsep_crc32c_batch_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_uint64]),
+    "kvsep_crc32c_batch_host_span": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                    ctypes.c_uint64]),
+    "kvsep_fill_splitmix64_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                                    ctypes.c_uint64]),
+    "kvsep_stream_read_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                ctypes.c_void_p]),
+    "kvsep_last_error": (ctypes.c_char_p, []),
+    "kvsep_build_info": (ctypes.c_char_p, []),
+    "kvsep_device_count": (ctypes.c_int, []),
+}
+
+
+def lib():
+    """Load libkvsep_crc32c.so (raises loudly if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise KvsepError(f"{LIB_PATH} missing: run `make -C kv-separate_amd` (or __graft_entry__.build())")
+        l = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = l
+    return _lib
+
+
+def header_functions(path: str = HEADER_PATH):
+    """Names of every function declared in include/kvsep_crc32c.h."""
+    src = open(path).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(kvsep_[a-z0-9_]+)\s*\(", src)))
+
+
+def _check(rc: int, what: str):
+    if rc != KVSEP_OK:
+        raise KvsepError(f"{what} failed ({rc}): {lib().kvsep_last_error().decode(errors='replace')}")
+
+
+def _buf(data):
+    """(ctypes pointer, keepalive) for bytes / bytearray / numpy arrays."""
+    if isinstance(data, np.ndarray):
+        a = np.ascontiguousarray(data)
+        return a.ctypes.data_as(ctypes.c_void_p), a
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        a = np.frombuffer(data, dtype=np.uint8)
+        return a.ctypes.data_as(ctypes.c_void_p), a
+    raise TypeError(type(data))
+
+
+# ------------------------------------------------------------------ scalar mirror of util/crc32c.h
+def extend(init_crc: int, data, n: int | None = None) -> int:
+    """leveldb::crc32c::Extend (util/crc32c.h:17)."""
+    p, keep = _buf(data)
+    n = keep.nbytes if n is None else n
+    return lib().kvsep_crc32c_extend(init_crc & 0xFFFFFFFF, p, n)
+
+
+def value(data, n: int | None = None) -> int:
+    """leveldb::crc32c::Value (util/crc32c.h:20)."""
+    return extend(0, data, n)
+
+
+def mask(crc: int) -> int:
+    """leveldb::crc32c::Mask (util/crc32c.h:29)."""
+    return lib().kvsep_crc32c_mask(crc & 0xFFFFFFFF)
+
+
+def unmask(masked: int) -> int:
+    """leveldb::crc32c::Unmask (util/crc32c.h:35)."""
+    return lib().kvsep_crc32c_unmask(masked & 0xFFFFFFFF)
+
+
+def extend_host(init_crc: int, data, n: int | None = None) -> int:
+    p, keep = _buf(data)
+    n = keep.nbytes if n is None else n
+    return lib().kvsep_crc32c_extend_host(init_crc & 0xFFFFFFFF, p, n)
+
+
+# ------------------------------------------------------------------ device context
+def _stream_handle(stream):
+    if stream is None:
+        if torch is not None and torch.cuda.is_available():
+            return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        return ctypes.c_void_p(0)
+    if hasattr(stream, "cuda_stream"):
+        return ctypes.c_void_p(stream.cuda_stream)
+    return ctypes.c_void_p(int(stream))
+
+
+def _dptr(t):
+    if t is None:
+        return ctypes.c_void_p(0)
+    if isinstance(t, int):
+        return ctypes.c_void_p(t)
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class Context:
+    """One per device: uploads the Z_d tables once, owns scratch and staging."""
+
+    def __init__(self, device: int = 0, piece_bytes: int | None = None, dynamic: bool | None = None):
+        h = ctypes.c_void_p()
+        _check(lib().kvsep_crc32c_ctx_create(device, ctypes.byref(h)), "kvsep_crc32c_ctx_create")
+        self._h = h
+        self.device = device
+        if piece_bytes is not None:
+            self.set_piece_bytes(piece_bytes)
+        if dynamic is not None:
+            self.set_schedule(dynamic)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().kvsep_crc32c_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_piece_bytes(self, n: int):
+        _check(lib().kvsep_crc32c_ctx_set_piece_bytes(self._h, n), "set_piece_bytes")
+
+    def set_schedule(self, dynamic: bool):
+        _check(lib().kvsep_crc32c_ctx_set_schedule(self._h, 1 if dynamic else 0), "set_schedule")
+
+    def reserve(self, count: int, total_bytes: int):
+        _check(lib().kvsep_crc32c_reserve(self._h, count, total_bytes), "reserve")
+
+    def set_timing(self, on: bool):
+        _check(lib().kvsep_crc32c_ctx_set_timing(self._h, 1 if on else 0), "set_timing")
+
+    def get_timing(self):
+        ms = ctypes.c_double()
+        n = ctypes.c_uint64()
+        _check(lib().kvsep_crc32c_ctx_get_timing(self._h, ctypes.byref(ms), ctypes.byref(n)), "get_timing")
+        return ms.value, n.value
+
+    # -- device form (torch tensors or raw device addresses)
+    def batch_device(self, base, off, length, out, init=None, count=None, total_bytes=None, max_len=0, stream=None):
+        count = int(off.numel()) if count is None else count
+        if total_bytes is None:
+            total_bytes = int(length.sum().item()) if count else 0
+        _check(lib().kvsep_crc32c_batch_device(self._h, _stream_handle(stream), _dptr(base), _dptr(off),
+                                               _dptr(length), _dptr(init), _dptr(out), count, total_bytes,
+                                               max_len), "kvsep_crc32c_batch_device")
+        return out
+
+    def verify_device(self, base, off, length, expected_masked, out, first_bad, nbad, init=None, count=None,
+                      total_bytes=None, max_len=0, stream=None):
+        count = int(off.numel()) if count is None else count
+        if total_bytes is None:
+            total_bytes = int(length.sum().item()) if count else 0
+        _check(lib().kvsep_crc32c_verify_device(self._h, _stream_handle(stream), _dptr(base), _dptr(off),
+                                                _dptr(length), _dptr(init), _dptr(expected_masked), _dptr(out),
+                                                _dptr(first_bad), _dptr(nbad), count, total_bytes, max_len),
+               "kvsep_crc32c_verify_device")
+        return out
+
+    def stream_read(self, src, nbytes: int, sink, stream=None):
+        _check(lib().kvsep_stream_read_device(self._h, _stream_handle(stream), _dptr(src), nbytes, _dptr(sink)),
+               "kvsep_stream_read_device")
+
+    # -- host forms (numpy / bytes)
+    def batch_host_span(self, buf, off, length, init=None):
+        p, keep = _buf(buf)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint64)
+        out = np.zeros(off.size, dtype=np.uint32)
+        ip = None
+        if init is not None:
+            init = np.ascontiguousarray(init, dtype=np.uint32)
+            ip = init.ctypes.data_as(ctypes.c_void_p)
+        _check(lib().kvsep_crc32c_batch_host_span(self._h, p, keep.nbytes, off.ctypes.data_as(ctypes.c_void_p),
+                                                  length.ctypes.data_as(ctypes.c_void_p), ip,
+                                                  out.ctypes.data_as(ctypes.c_void_p), off.size),
+               "kvsep_crc32c_batch_host_span")
+        return out
+
+    def batch_host(self, blocks, init=None):
+        """blocks: list of bytes-like objects (gathered through pinned staging)."""
+        keep = [_buf(b) for b in blocks]
+        n = len(blocks)
+        ptrs = (ctypes.c_void_p * n)(*[k[0].value for k in keep])
+        lens = np.array([k[1].nbytes for k in keep], dtype=np.uint64)
+        out = np.zeros(n, dtype=np.uint32)
+        ip = None
+        if init is not None:
+            init = np.ascontiguousarray(init, dtype=np.uint32)
+            ip = init.ctypes.data_as(ctypes.c_void_p)
+        _check(lib().kvsep_crc32c_batch_host(self._h, ip, ptrs, lens.ctypes.data_as(ctypes.c_void_p),
+                                             out.ctypes.data_as(ctypes.c_void_p), n), "kvsep_crc32c_batch_host")
+        return out
+
+
+def fill_splitmix64(dst, nbytes: int, seed: int, stream_offset: int = 0, stream=None):
+    """Device synthetic data (same stream as oracle_fill_splitmix64 / splitmix64_bytes below)."""
+    _check(lib().kvsep_fill_splitmix64_device(_stream_handle(stream), _dptr(dst), nbytes, seed & (2**64 - 1),
+                                              stream_offset), "kvsep_fill_splitmix64_device")
+
+
+def splitmix64_bytes(nbytes: int, seed: int, stream_offset: int = 0) -> np.ndarray:
+    """Host (numpy) version of the synthetic byte stream, for small test cases."""
+    w0 = stream_offset >> 3
+    w1 = (stream_offset + nbytes + 7) >> 3
+    j = np.arange(w0, w1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + (j + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    b = z.astype("<u8").view(np.uint8)
+    s = stream_offset - (w0 << 3)
+    return b[s:s + nbytes].copy()
+
+
+def device_count() -> int:
+    return lib().kvsep_device_count()
+
+
+def build_info() -> str:
+    return lib().kvsep_build_info().decode()

@@ -1,0 +1,261 @@
+"""GPU parity: the HIP path (through the C ABI) vs golden vectors from the compiled reference and
+vs the oracle restatement, bit-exact.  Needs a gfx950 device (`-m gpu`)."""
+import numpy as np
+import pytest
+
+import kvsep
+from kvsep import splitmix64_bytes
+from kvsep import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no GPU", allow_module_level=True)
+
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = kvsep.Context(0)
+    yield c
+    c.close()
+
+
+def dev_u64(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64)).to(DEV)
+
+
+def dev_u32(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32)).to(DEV)
+
+
+def dev_bytes(a, pad=64):
+    t = torch.zeros(a.size + pad, dtype=torch.uint8, device=DEV)
+    if a.size:
+        t[:a.size] = torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint8)).to(DEV)
+    return t
+
+
+def run(ctx, data_t, off, ln, init=None, max_len=0, base_shift=0):
+    out = torch.zeros(len(off), dtype=torch.int32, device=DEV)
+    ctx.batch_device(data_t.data_ptr() + base_shift, dev_u64(off), dev_u64(ln), out,
+                     init=None if init is None else dev_u32(init), max_len=max_len,
+                     total_bytes=int(np.sum(ln, dtype=np.uint64)))
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("piece", [256 * 1024, 1024])
+@pytest.mark.parametrize("dynamic", [True, False])
+def test_sweep_every_offset_and_length(ctx, golden, piece, dynamic):
+    ctx.set_piece_bytes(piece)
+    ctx.set_schedule(dynamic)
+    sw = golden["sweep"]
+    d = dev_bytes(splitmix64_bytes(4096, sw["seed"], 0))
+    o, n = np.meshgrid(np.arange(16), np.arange(257), indexing="ij")
+    off, ln = o.ravel().astype(np.uint64), n.ravel().astype(np.uint64)
+    exp0 = np.array(sw["crc_init0"], dtype=np.uint32).ravel()
+    expi = np.array(sw["crc_init"], dtype=np.uint32).ravel()
+    init = np.array(sw["init"], dtype=np.uint32).ravel()
+    for max_len in (0, 256):
+        assert np.array_equal(run(ctx, d, off, ln, max_len=max_len), exp0)
+        assert np.array_equal(run(ctx, d, off, ln, init, max_len=max_len), expi)
+    ctx.set_piece_bytes(256 * 1024)
+    ctx.set_schedule(True)
+
+
+@pytest.mark.parametrize("piece", [256 * 1024, 4096, 1024, 1 << 20])
+def test_large_blocks_golden(ctx, golden, piece):
+    ctx.set_piece_bytes(piece)
+    d = dev_bytes(splitmix64_bytes((4 << 20) + 64, W.SEED + 1, 0))
+    cases = golden["large"]
+    off = np.array([c["offset"] for c in cases], np.uint64)
+    ln = np.array([c["len"] for c in cases], np.uint64)
+    init = np.array([c["init"] for c in cases], np.uint32)
+    exp = np.array([c["crc"] for c in cases], np.uint32)
+    assert np.array_equal(run(ctx, d, off, ln, init), exp)
+    assert np.array_equal(run(ctx, d, off, ln, init, max_len=int(ln.max())), exp)
+    ctx.set_piece_bytes(256 * 1024)
+
+
+def test_known_vectors(ctx, golden):
+    blobs = []
+    for k in golden["known"]:
+        blobs.append(bytes.fromhex(k["hex"]) if k["hex"] is not None else bytes([k["fill"]["byte"]]) * k["fill"]["n"])
+    lens = np.array([len(b) for b in blobs], np.uint64)
+    off = np.zeros(len(blobs), np.uint64)
+    off[1:] = np.cumsum(lens[:-1])
+    d = dev_bytes(np.frombuffer(b"".join(blobs), np.uint8))
+    got = run(ctx, d, off, lens)
+    assert got.tolist() == [k["value"] for k in golden["known"]]
+    ke = golden["known_extend"]
+    d2 = dev_bytes(np.frombuffer(ke["data"].encode(), np.uint8))
+    assert run(ctx, d2, np.zeros(1, np.uint64), np.array([5], np.uint64), np.array([ke["init"]], np.uint32))[0] == ke["value"]
+
+
+def test_device_generator_matches_host_stream():
+    for so, n in ((0, 4096), (16, 1000), (5, 333)):
+        t = torch.zeros(n + 32, dtype=torch.uint8, device=DEV)
+        kvsep.fill_splitmix64(t.data_ptr(), n, W.SEED, so)
+        torch.cuda.synchronize()
+        assert np.array_equal(t[:n].cpu().numpy(), splitmix64_bytes(n, W.SEED, so))
+
+
+def test_cfg2_full_batch(ctx, golden):
+    g = golden["cfg2"]
+    off, ln = W.cfg2_layout()
+    total = int(ln.sum())
+    d = torch.empty(total + 64, dtype=torch.uint8, device=DEV)
+    kvsep.fill_splitmix64(d.data_ptr(), total, g["seed"], 0)
+    for max_len in (4096, 0):
+        got = run(ctx, d, off, ln, max_len=max_len)
+        assert got[:256].tolist() == g["first"]
+        assert int(np.bitwise_xor.reduce(got)) == g["xor"]
+        assert int(got.astype(np.uint64).sum()) == g["sum"]
+        assert kvsep.extend_host(0, got.tobytes()) == g["crc_of_crcs"]
+
+
+def test_cfg3b_vlog_prefix(ctx, golden):
+    g = golden["cfg3b"]
+    off, ln = W.cfg3_layout(vlog=True, count=g["count"])
+    span = int(off[-1] + ln[-1])
+    d = torch.empty(span + 64, dtype=torch.uint8, device=DEV)
+    kvsep.fill_splitmix64(d.data_ptr(), span, g["seed"], 0)
+    for max_len in (0, W.VLOG_PAYLOAD):
+        assert run(ctx, d, off, ln, max_len=max_len).tolist() == g["crc"]
+
+
+def test_cfg4_prefix_golden(ctx, golden):
+    g = golden["cfg4"]
+    off, ln = W.cfg4_layout(g["count"])
+    span = int(off[-1] + ln[-1])
+    d = torch.empty(span + 64, dtype=torch.uint8, device=DEV)
+    kvsep.fill_splitmix64(d.data_ptr(), span, g["seed"], 0)
+    assert run(ctx, d, off, ln).tolist() == g["crc"]
+
+
+def test_cfg4_ragged_sample_vs_oracle(ctx, oracle):
+    off, ln = W.cfg4_layout(8192)
+    span = int(off[-1] + ln[-1])
+    d = torch.empty(span + 64, dtype=torch.uint8, device=DEV)
+    kvsep.fill_splitmix64(d.data_ptr(), span, W.SEED + 2, 0)
+    host = d[:span].cpu().numpy()
+    exp = oracle.batch(host, off, ln, threads=16)
+    for piece in (256 * 1024, 64 * 1024, 1 << 20):
+        ctx.set_piece_bytes(piece)
+        for dyn in (True, False):
+            ctx.set_schedule(dyn)
+            assert np.array_equal(run(ctx, d, off, ln), exp), (piece, dyn)
+    ctx.set_piece_bytes(256 * 1024)
+    ctx.set_schedule(True)
+
+
+def test_random_blocks_many_pieces_vs_oracle(ctx, oracle):
+    rng = np.random.default_rng(5)
+    n = 3000
+    data = splitmix64_bytes(1 << 22, 99, 0)
+    ln = rng.integers(0, 40000, n).astype(np.uint64)
+    ln[:50] = rng.integers(0, 40, 50)
+    off = rng.integers(0, data.size - 40000, n).astype(np.uint64)  # overlapping, any alignment
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    d = dev_bytes(data)
+    exp = oracle.batch(data, off, ln, init, threads=8)
+    for piece in (1024, 3072, 8192, 256 * 1024):
+        ctx.set_piece_bytes(piece)
+        assert np.array_equal(run(ctx, d, off, ln, init), exp), piece
+    ctx.set_piece_bytes(256 * 1024)
+
+
+def test_edge_cases(ctx):
+    d = dev_bytes(splitmix64_bytes(4096, 3, 0))
+    # empty batch is a no-op
+    out = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ctx.batch_device(d.data_ptr(), dev_u64([0]), dev_u64([0]), out, count=0, total_bytes=0)
+    torch.cuda.synchronize()
+    # zero-length blocks return init unchanged (util/crc32c.cc:276 with n == 0)
+    init = np.array([0, 0x12345678, 0xFFFFFFFF], np.uint32)
+    assert run(ctx, d, np.zeros(3, np.uint64), np.zeros(3, np.uint64), init).tolist() == init.tolist()
+    # a block at the very start of the allocation, odd offsets at its end
+    assert run(ctx, d, np.array([0], np.uint64), np.array([4095], np.uint64))[0] == \
+        kvsep.extend_host(0, d[:4095].cpu().numpy())
+
+
+def test_block_longer_than_4gib_boundary(ctx, oracle):
+    """One 2^32+77-byte block at an odd offset: 64-bit offsets/lengths, many pieces."""
+    n = (1 << 32) + 77
+    d = torch.empty(n + 64, dtype=torch.uint8, device=DEV)
+    kvsep.fill_splitmix64(d.data_ptr(), n + 64, 11, 0)
+    got = run(ctx, d, np.array([3], np.uint64), np.array([n], np.uint64), np.array([0xABCDEF01], np.uint32))[0]
+    host = d[3:3 + n].cpu().numpy()
+    assert got == oracle.extend_addr(0xABCDEF01, host.ctypes.data, n)
+    del d
+
+
+def test_verify_mode_first_bad(ctx, oracle):
+    """db/value_log_reader.cc:109-123: Mask(Value(payload)) == stored; scan stops at first mismatch."""
+    off, ln = W.cfg3_layout(vlog=True, count=64)
+    span = int(off[-1] + ln[-1])
+    d = torch.empty(span + 64, dtype=torch.uint8, device=DEV)
+    kvsep.fill_splitmix64(d.data_ptr(), span, 5, 0)
+    host = d[:span].cpu().numpy()
+    crc = oracle.batch(host, off, ln, threads=16)
+    expected = np.array([oracle.lib.oracle_crc32c_mask(int(c)) for c in crc], np.uint32)
+    out = torch.zeros(64, dtype=torch.int32, device=DEV)
+    fb = torch.zeros(1, dtype=torch.int64, device=DEV)
+    nb = torch.zeros(1, dtype=torch.int64, device=DEV)
+    ctx.verify_device(d.data_ptr(), dev_u64(off), dev_u64(ln), dev_u32(expected), out, fb, nb)
+    torch.cuda.synchronize()
+    assert fb.item() == -1 and nb.item() == 0  # UINT64_MAX
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), crc)
+    d[int(off[41]) + 1000] ^= 0x80  # corruption_test.cc style bit flip
+    d[int(off[57]) + 7] ^= 0x01
+    ctx.verify_device(d.data_ptr(), dev_u64(off), dev_u64(ln), dev_u32(expected), out, fb, nb)
+    torch.cuda.synchronize()
+    assert fb.item() == 41 and nb.item() == 2
+
+
+def test_host_span_and_gather_forms(ctx, oracle):
+    off, ln = W.cfg4_layout(3000)
+    span = int(off[-1] + ln[-1])
+    data = splitmix64_bytes(span, 17, 0)
+    init = (np.arange(3000, dtype=np.uint64) * 2654435761 % (2**32)).astype(np.uint32)
+    exp = oracle.batch(data, off, ln, init, threads=16)
+    assert np.array_equal(ctx.batch_host_span(data, off, ln, init), exp)
+    blocks = [data[int(o):int(o + l)].tobytes() for o, l in zip(off[:500], ln[:500])]
+    assert np.array_equal(ctx.batch_host(blocks, init[:500]), exp[:500])
+
+
+def test_host_span_block_larger_than_staging(ctx, oracle):
+    n = (150 << 20) + 13
+    data = splitmix64_bytes(n + 16, 23, 0)
+    off = np.array([3, 1], np.uint64)
+    ln = np.array([n, 1000], np.uint64)
+    exp = oracle.batch(data, off, ln, np.array([7, 9], np.uint32), threads=2)
+    assert np.array_equal(ctx.batch_host_span(data, off, ln, np.array([7, 9], np.uint32)), exp)
+
+
+def test_dropin_extend_offload_path(golden):
+    kvsep.lib().kvsep_set_offload_threshold(0)  # force every Extend through the GPU
+    try:
+        for k in golden["known"]:
+            dat = bytes.fromhex(k["hex"]) if k["hex"] is not None else bytes([k["fill"]["byte"]]) * k["fill"]["n"]
+            assert kvsep.value(dat) == k["value"], k["name"]
+        assert kvsep.lib().kvsep_accelerated_crc32c(0, b"TestCRCBuffer", 13) == 0xDCBC59FA
+        assert kvsep.value(b"hello world") == kvsep.extend(kvsep.value(b"hello "), b"world")
+    finally:
+        kvsep.lib().kvsep_set_offload_threshold(64 << 20)
+
+
+def test_split_invariance_full_cfg3_scale(ctx):
+    """Size-independent property on 2048 x 1 MiB: CRC(block) == Extend(CRC(first k bytes), rest)."""
+    off, ln = W.cfg3_layout(count=2048)
+    total = int(ln.sum())
+    d = torch.empty(total + 64, dtype=torch.uint8, device=DEV)
+    kvsep.fill_splitmix64(d.data_ptr(), total, W.SEED + 1, 0)
+    whole = run(ctx, d, off, ln, max_len=1 << 20)
+    k = (np.arange(2048, dtype=np.uint64) * 7919) % (1 << 20)
+    first = run(ctx, d, off, k)
+    rest = run(ctx, d, off + k, ln - k, first)
+    assert np.array_equal(whole, rest)
