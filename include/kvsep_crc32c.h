@@ -56,7 +56,8 @@ int kvsep_crc32c_ctx_create(int device, kvsep_crc32c_ctx** out);
 void kvsep_crc32c_ctx_destroy(kvsep_crc32c_ctx* ctx);
 /* Work-item ("piece") size for splitting long blocks; default 256 KiB, min 1 KiB, multiple of 1 KiB. */
 int kvsep_crc32c_ctx_set_piece_bytes(kvsep_crc32c_ctx* ctx, uint64_t piece_bytes);
-/* 0 = static round-robin of pieces over waves, 1 = dynamic (atomic work counter). Default 1. */
+/* 0 = static round-robin of work items over waves, 1 = guided dynamic (one atomic per run of items),
+ * -1 = auto (default): guided when long blocks are split into pieces, else static. */
 int kvsep_crc32c_ctx_set_schedule(kvsep_crc32c_ctx* ctx, int dynamic);
 /* Pre-size scratch so later calls of up to `count` blocks / `total_bytes` bytes do not allocate
  * (required before graph capture). */

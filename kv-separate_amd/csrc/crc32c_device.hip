@@ -124,16 +124,24 @@ __device__ __forceinline__ uint32_t serial16(const uint8_t* lds, uint32_t reg, u
 }
 
 // Global (not flat) address space: flat loads would tie the LDS counter to every data load.
+// Streamed payload is read once: non-temporal loads (kNT) keep it from displacing anything useful and
+// measured 6.2 -> 7.0 TB/s on this access pattern (kv-separate_amd/tools/hbm_probe.hip).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) u32x4 gu32x4;
+template <bool kNT = false>
 __device__ __forceinline__ uint4 ld16(uintptr_t addr) {
-  const u32x4 v = *reinterpret_cast<gu32x4*>(addr);
+  gu32x4* g = reinterpret_cast<gu32x4*>(addr);
+  u32x4 v;
+  if constexpr (kNT) v = __builtin_nontemporal_load(g);
+  else v = *g;
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
 // Raw CRC register after consuming [ps, pe) starting from register `reg` (no final inversion).
-__device__ __forceinline__ uint32_t crc_piece(const uint8_t* lds, uintptr_t ps, uintptr_t pe, uint32_t reg, uint32_t lane,
-                              uint32_t lc0, uint32_t lc1) {
+// kG rows are computed while the next kG rows are in flight.
+template <int kG, bool kNT>
+__device__ __forceinline__ uint32_t crc_piece(const uint8_t* lds, uintptr_t ps, uintptr_t pe, uint32_t reg,
+                                              uint32_t lane, uint32_t lc0, uint32_t lc1) {
   const uintptr_t hbase = ps & ~uintptr_t(15);
   uintptr_t h0 = (ps + 15) & ~uintptr_t(15);
   if (h0 > pe) h0 = pe;
@@ -150,14 +158,14 @@ __device__ __forceinline__ uint32_t crc_piece(const uint8_t* lds, uintptr_t ps, 
     const uintptr_t seg = rb + uintptr_t(lane) * 16u;
     // issue the first rows' loads before the serial head work
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (seg >= h0) v = ld16(seg);  // row 0 is front-masked: lanes before h0 hold zeros
-    const uint64_t ngroups = (K - 1) >> 2;
-    uint4 A0, A1, A2, A3;
-    if (ngroups) {
-      A0 = ld16(seg + 1 * kRowBytes);
-      A1 = ld16(seg + 2 * kRowBytes);
-      A2 = ld16(seg + 3 * kRowBytes);
-      A3 = ld16(seg + 4 * kRowBytes);
+    if (seg >= h0) v = ld16<kNT>(seg);  // row 0 is front-masked: lanes before h0 hold zeros
+    // A holds rows r .. r+kG-1 (clamped to the last row); all issued before any compute, so a short
+    // piece (a 4 KiB block has 3 rows after row 0) has every row in flight at once.
+    const uint64_t last = K - 1;
+    uint4 A[kG];
+    if (K > 1) {
+#pragma unroll
+      for (int i = 0; i < kG; ++i) A[i] = ld16<kNT>(seg + (1 + i < last ? 1 + i : last) * kRowBytes);
     }
     if (ps < h0) reg = serial16(lds, reg, hc, int(ps - hbase), int(h0 - hbase));
     if (seg == h0) v.x ^= reg;  // the head register enters as pending word at h0
@@ -172,24 +180,19 @@ __device__ __forceinline__ uint32_t crc_piece(const uint8_t* lds, uintptr_t ps, 
   } while (0)
 
     uint64_t r = 1;
-    const uint64_t last = K - 1;
-    for (uint64_t g = 0; g < ngroups; ++g) {
-      const uint64_t nr = r + 4;  // prefetch the next group (clamped: re-reads of the last row are harmless)
-      const uint4 B0 = ld16(seg + (nr + 0 < last ? nr + 0 : last) * kRowBytes);
-      const uint4 B1 = ld16(seg + (nr + 1 < last ? nr + 1 : last) * kRowBytes);
-      const uint4 B2 = ld16(seg + (nr + 2 < last ? nr + 2 : last) * kRowBytes);
-      const uint4 B3 = ld16(seg + (nr + 3 < last ? nr + 3 : last) * kRowBytes);
-      KVSEP_ROW(A0);
-      KVSEP_ROW(A1);
-      KVSEP_ROW(A2);
-      KVSEP_ROW(A3);
-      A0 = B0; A1 = B1; A2 = B2; A3 = B3;
-      r = nr;
+    for (; r + kG <= K; r += kG) {  // full group in A: compute it while the next group loads
+      uint4 B[kG];
+      const uint64_t nr = r + kG;
+#pragma unroll
+      for (int i = 0; i < kG; ++i) B[i] = ld16<kNT>(seg + (nr + i < last ? nr + i : last) * kRowBytes);
+#pragma unroll
+      for (int i = 0; i < kG; ++i) KVSEP_ROW(A[i]);
+#pragma unroll
+      for (int i = 0; i < kG; ++i) A[i] = B[i];
     }
-    for (; r < K; ++r) {
-      const uint4 V = ld16(seg + r * kRowBytes);
-      KVSEP_ROW(V);
-    }
+#pragma unroll
+    for (int i = 0; i < kG; ++i)  // remainder rows r .. K-1, already in A
+      if (r + i < K) KVSEP_ROW(A[i]);
 #undef KVSEP_ROW
     // lane merge: pending word at (16*lane + 12) of the last row
     uint32_t p = zmap(lds, kZ4Off, c0) ^ c1;
@@ -221,7 +224,7 @@ __device__ __forceinline__ void emit_block(const PiecesArgs& a, uint64_t b, uint
   }
 }
 
-template <bool kPlanned, bool kDynamic>
+template <bool kPlanned, bool kDynamic, int kG, bool kNT>
 __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   const uint32_t tid = threadIdx.x;
@@ -252,53 +255,59 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
     if (total > a.max_pieces) total = a.max_pieces;  // scratch overflow guard (caller bound violated)
   }
 
-  uint64_t g;
-  if (kDynamic) {
-    uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(a.work_counter, 1u);
-    g = __builtin_amdgcn_readfirstlane(t);
-  } else {
-    g = uint64_t(blockIdx.x) * kWavesPerWg + wave;
-  }
-
-  while (g < total) {
-    uint64_t gn;
-    if (kDynamic) {  // fetch the next ticket while this piece is processed
+  // Work distribution.  Static: wave w takes items w, w + nwaves, ...  Dynamic ("guided"): a wave
+  // grabs a run of max(1, remaining / (4 * nwaves)) consecutive items with ONE atomic, so early
+  // grabs are long and the tail is single items -- far below the ~88 dequeues/us one counter serves.
+  uint64_t lo, hi;
+  uint64_t seen = 0;  // dynamic: counter value this wave last observed
+  auto grab = [&](uint64_t& l, uint64_t& h) {
+    if (kDynamic) {
+      const uint64_t rem = total > seen ? total - seen : 0;
+      uint64_t c = rem / (4 * nwaves);
+      if (c < 1) c = 1;
+      if (c > 0xffffffffull) c = 0xffffffffull;
       uint32_t t = 0;
-      if (lane == 0) t = atomicAdd(a.work_counter, 1u);
-      gn = __builtin_amdgcn_readfirstlane(t);
+      if (lane == 0) t = atomicAdd(a.work_counter, uint32_t(c));
+      l = __builtin_amdgcn_readfirstlane(t);
+      h = l + c < total ? l + c : total;
+      seen = l + c;
     } else {
-      gn = g + nwaves;
+      l = (l == ~uint64_t(0)) ? uint64_t(blockIdx.x) * kWavesPerWg + wave : l + nwaves;
+      h = l + 1;
     }
-    uint64_t b;
-    uint64_t rs, re;
-    bool first, only;
-    const uint64_t n_b = 0;
-    (void)n_b;
-    if (kPlanned) {
-      b = a.pblk[g];
-      const uint64_t s = a.pstart[b], k = uint64_t(a.pstart[b + 1]) - s, j = g - s;
-      const uint64_t n = a.len[b];
-      re = n - (k - 1 - j) * a.piece_bytes;
-      rs = j ? n - (k - j) * a.piece_bytes : 0;
-      first = (j == 0);
-      only = (k == 1);
-    } else {
-      b = g;
-      rs = 0;
-      re = a.len[b];
-      first = true;
-      only = true;
+  };
+  lo = ~uint64_t(0);
+  grab(lo, hi);
+  while (lo < total) {
+    for (uint64_t g = lo; g < hi; ++g) {
+      uint64_t b;
+      uint64_t rs, re;
+      bool first, only;
+      if (kPlanned) {
+        b = a.pblk[g];
+        const uint64_t s0 = a.pstart[b], k = uint64_t(a.pstart[b + 1]) - s0, j = g - s0;
+        const uint64_t n = a.len[b];
+        re = n - (k - 1 - j) * a.piece_bytes;
+        rs = j ? n - (k - j) * a.piece_bytes : 0;
+        first = (j == 0);
+        only = (k == 1);
+      } else {
+        b = g;
+        rs = 0;
+        re = a.len[b];
+        first = true;
+        only = true;
+      }
+      const uintptr_t blk = reinterpret_cast<uintptr_t>(a.base) + a.off[b];
+      uint32_t reg0 = 0;
+      if (first) reg0 = ~(a.init ? a.init[b] : 0u);
+      const uint32_t reg = crc_piece<kG, kNT>(lds, blk + rs, blk + re, reg0, lane, lc0, lc1);
+      if (lane == 0) {
+        if (only) emit_block(a, b, ~reg);
+        else a.partial[g] = reg;
+      }
     }
-    const uintptr_t blk = reinterpret_cast<uintptr_t>(a.base) + a.off[b];
-    uint32_t reg0 = 0;
-    if (first) reg0 = ~(a.init ? a.init[b] : 0u);
-    const uint32_t reg = crc_piece(lds, blk + rs, blk + re, reg0, lane, lc0, lc1);
-    if (lane == 0) {
-      if (only) emit_block(a, b, ~reg);
-      else a.partial[g] = reg;
-    }
-    g = gn;
+    grab(lo, hi);
   }
 }
 
@@ -359,16 +368,27 @@ __global__ void fill_splitmix_bytes_kernel(uint8_t* dst, uint64_t n, uint64_t se
   }
 }
 
-__global__ void __launch_bounds__(256) stream_read_kernel(const uint4* src, uint64_t n16, uint32_t* sink) {
+// The attainable-read ceiling for the same access pattern as the CRC kernel: each wave streams its own
+// contiguous 1 MiB chunk as 1 KiB rows, 8 rows in flight, non-temporal loads (hbm_probe's best pattern).
+__global__ void __launch_bounds__(1024) stream_read_kernel(uintptr_t src, uint64_t n16, uint32_t* sink) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wave = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = (uint64_t(gridDim.x) * blockDim.x) >> 6;
+  constexpr uint64_t kChunk16 = (1u << 20) / 16;
+  const uint64_t nchunks = n16 / kChunk16;
   uint32_t acc = 0;
-  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-  uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  for (; i + 3 * stride < n16; i += 4 * stride) {
-    const uint4 x0 = src[i], x1 = src[i + stride], x2 = src[i + 2 * stride], x3 = src[i + 3 * stride];
-    acc ^= x0.x ^ x0.y ^ x0.z ^ x0.w ^ x1.x ^ x1.y ^ x1.z ^ x1.w ^ x2.x ^ x2.y ^ x2.z ^ x2.w ^ x3.x ^ x3.y ^ x3.z ^ x3.w;
+  for (uint64_t c = wave; c < nchunks; c += nwaves) {
+    const uintptr_t p = src + (c * kChunk16 + lane) * 16;
+    for (uint64_t r = 0; r < kChunk16 * 16; r += 8 * kRowBytes) {
+      uint4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = ld16<true>(p + r + u * kRowBytes);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
   }
-  for (; i < n16; i += stride) {
-    const uint4 x = src[i];
+  for (uint64_t i = nchunks * kChunk16 + wave * 64 + lane; i < n16; i += nwaves * 64) {
+    const uint4 x = ld16<true>(src + i * 16);
     acc ^= x.x ^ x.y ^ x.z ^ x.w;
   }
   if (acc == 0x9e3779b9u) atomicXor(sink, acc);  // keeps the loads live; practically never stores
@@ -385,7 +405,8 @@ struct kvsep_crc32c_ctx {
   int num_cus = 0;
   DevTables* d_tabs = nullptr;
   uint64_t piece_bytes = 256 * 1024;
-  int dynamic = 1;
+  int dynamic = -1;  // -1 auto, 0 static, 1 guided
+  int variant = 1;   // rows per prefetch group / load policy, see launch_pieces
   // scratch
   uint64_t cap_count = 0, cap_pieces = 0;
   uint32_t* d_counts = nullptr;
@@ -476,6 +497,26 @@ hipEvent_t take_event(kvsep_crc32c_ctx* c) {
   return e;
 }
 
+template <bool P, bool D>
+void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs& a) {
+  switch (variant) {  // 0: 4 rows, plain loads  1: 4 rows, non-temporal  2: 8 rows, non-temporal  3: 8 rows plain
+    case 0: crc32c_pieces_kernel<P, D, 4, false><<<grid, kWgThreads, 0, s>>>(a); break;
+    case 1: crc32c_pieces_kernel<P, D, 4, true><<<grid, kWgThreads, 0, s>>>(a); break;
+    case 3: crc32c_pieces_kernel<P, D, 8, false><<<grid, kWgThreads, 0, s>>>(a); break;
+    default: crc32c_pieces_kernel<P, D, 8, true><<<grid, kWgThreads, 0, s>>>(a); break;
+  }
+}
+
+void launch_pieces(bool planned, bool dyn, int variant, unsigned grid, hipStream_t s, const PiecesArgs& a) {
+  if (planned) {
+    if (dyn) launch_pieces_v<true, true>(variant, grid, s, a);
+    else launch_pieces_v<true, false>(variant, grid, s, a);
+  } else {
+    if (dyn) launch_pieces_v<false, true>(variant, grid, s, a);
+    else launch_pieces_v<false, false>(variant, grid, s, a);
+  }
+}
+
 int launch_batch(kvsep_crc32c_ctx* c, hipStream_t s, const void* base, const uint64_t* off, const uint64_t* len,
                  const uint32_t* init, const uint32_t* expect, uint32_t* out, uint64_t* first_bad, uint64_t* nbad,
                  uint64_t count, uint64_t total_bytes, uint64_t max_len) {
@@ -522,7 +563,8 @@ int launch_batch(kvsep_crc32c_ctx* c, hipStream_t s, const void* base, const uin
   } else {
     a.max_pieces = count;
   }
-  if (c->dynamic) {
+  const bool dyn = c->dynamic < 0 ? planned : c->dynamic == 1;  // auto: guided when planned, else static
+  if (dyn) {
     if (!c->d_counter) KVSEP_HIP(hipMalloc(&c->d_counter, 16));
     a.work_counter = c->d_counter;
     KVSEP_HIP(hipMemsetAsync(c->d_counter, 0, 4, s));
@@ -534,13 +576,7 @@ int launch_batch(kvsep_crc32c_ctx* c, hipStream_t s, const void* base, const uin
     e1 = take_event(c);
     if (e0 && e1) KVSEP_HIP(hipEventRecord(e0, s));
   }
-  if (planned) {
-    if (c->dynamic) crc32c_pieces_kernel<true, true><<<grid, kWgThreads, 0, s>>>(a);
-    else crc32c_pieces_kernel<true, false><<<grid, kWgThreads, 0, s>>>(a);
-  } else {
-    if (c->dynamic) crc32c_pieces_kernel<false, true><<<grid, kWgThreads, 0, s>>>(a);
-    else crc32c_pieces_kernel<false, false><<<grid, kWgThreads, 0, s>>>(a);
-  }
+  launch_pieces(planned, dyn, c->variant, grid, s, a);
   KVSEP_HIP(hipGetLastError());
   if (c->timing && e0 && e1) {
     KVSEP_HIP(hipEventRecord(e1, s));
@@ -590,6 +626,7 @@ int kvsep_crc32c_ctx_create(int device, kvsep_crc32c_ctx** out) {
   auto* c = new kvsep_crc32c_ctx();
   c->device = device;
   c->num_cus = prop.multiProcessorCount;
+  if (const char* v = std::getenv("KVSEP_CRC_VARIANT")) c->variant = std::atoi(v);
   KVSEP_HIP(hipSetDevice(device));
   int rc = upload_tables(c);
   if (rc) {
@@ -626,7 +663,7 @@ int kvsep_crc32c_ctx_set_piece_bytes(kvsep_crc32c_ctx* c, uint64_t piece_bytes) 
 
 int kvsep_crc32c_ctx_set_schedule(kvsep_crc32c_ctx* c, int dynamic) {
   if (!c) return set_err(KVSEP_EINVAL, "null ctx");
-  c->dynamic = dynamic ? 1 : 0;
+  c->dynamic = dynamic < 0 ? -1 : (dynamic ? 1 : 0);
   return KVSEP_OK;
 }
 
@@ -712,7 +749,7 @@ int kvsep_stream_read_device(kvsep_crc32c_ctx* c, void* stream, const void* src,
     e1 = take_event(c);
     if (e0 && e1) KVSEP_HIP(hipEventRecord(e0, s));
   }
-  stream_read_kernel<<<unsigned(c->num_cus) * 8, 256, 0, s>>>(static_cast<const uint4*>(src), n16, sink);
+  stream_read_kernel<<<unsigned(c->num_cus), 1024, 0, s>>>(reinterpret_cast<uintptr_t>(src), n16, sink);
   KVSEP_HIP(hipGetLastError());
   if (c->timing && e0 && e1) {
     KVSEP_HIP(hipEventRecord(e1, s));

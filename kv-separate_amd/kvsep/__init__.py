@@ -194,8 +194,10 @@ class Context:
     def set_piece_bytes(self, n: int):
         _check(lib().kvsep_crc32c_ctx_set_piece_bytes(self._h, n), "set_piece_bytes")
 
-    def set_schedule(self, dynamic: bool):
-        _check(lib().kvsep_crc32c_ctx_set_schedule(self._h, 1 if dynamic else 0), "set_schedule")
+    def set_schedule(self, dynamic):
+        """True = guided dynamic, False = static, None = auto (guided only when long blocks are split)."""
+        v = -1 if dynamic is None else (1 if dynamic else 0)
+        _check(lib().kvsep_crc32c_ctx_set_schedule(self._h, v), "set_schedule")
 
     def reserve(self, count: int, total_bytes: int):
         _check(lib().kvsep_crc32c_reserve(self._h, count, total_bytes), "reserve")

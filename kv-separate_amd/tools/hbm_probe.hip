@@ -1,0 +1,162 @@
+// hbm_probe.hip -- measurement tool (not part of the library): which read pattern gets closest to the
+// MI355X HBM peak?  Times read-only kernels over a large buffer with hipEvents and prints GB/s.
+// Build: hipcc --offload-arch=gfx950 -O3 -o hbm_probe hbm_probe.hip ; run: ./hbm_probe [GiB]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4 gu32x4;
+
+#define CHECK(x)                                                                   \
+  do {                                                                             \
+    hipError_t e = (x);                                                            \
+    if (e != hipSuccess) {                                                         \
+      printf("%s failed: %s\n", #x, hipGetErrorString(e));                         \
+      exit(1);                                                                     \
+    }                                                                              \
+  } while (0)
+
+template <int U, bool NT>
+__device__ __forceinline__ u32x4 ld(const u32x4* p) {
+  gu32x4* g = reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(p));
+  if constexpr (NT) return __builtin_nontemporal_load(g);
+  return *g;
+}
+
+// A: grid-stride, U independent loads in flight per thread
+template <int U, bool NT>
+__global__ void k_gridstride(const u32x4* src, size_t n16, unsigned* sink) {
+  u32x4 acc = {0, 0, 0, 0};
+  const size_t stride = size_t(gridDim.x) * blockDim.x;
+  size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (; i + (U - 1) * stride < n16; i += U * stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld<U, NT>(src + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u];
+  }
+  for (; i < n16; i += stride) acc ^= ld<U, NT>(src + i);
+  unsigned a = acc.x ^ acc.y ^ acc.z ^ acc.w;
+  if (a == 0x12345678u) atomicXor(sink, a);
+}
+
+// B: each wave owns a contiguous chunk of `chunk16` x 16 B, read as 1 KiB rows, U rows in flight.
+template <int U, bool NT>
+__global__ void k_wavechunk(const u32x4* src, size_t n16, size_t chunk16, unsigned* sink) {
+  const unsigned lane = threadIdx.x & 63;
+  const size_t wave = (size_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const size_t nwaves = (size_t(gridDim.x) * blockDim.x) >> 6;
+  u32x4 acc = {0, 0, 0, 0};
+  const size_t nchunks = n16 / chunk16;
+  for (size_t c = wave; c < nchunks; c += nwaves) {
+    const u32x4* p = src + c * chunk16 + lane;
+    for (size_t r = 0; r < chunk16; r += 64 * U) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ld<U, NT>(p + r + 64 * u);
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc ^= v[u];
+    }
+  }
+  unsigned a = acc.x ^ acc.y ^ acc.z ^ acc.w;
+  if (a == 0x12345678u) atomicXor(sink, a);
+}
+
+// C: each workgroup owns a contiguous chunk; its waves interleave rows (wave w reads rows w, w+W, ...).
+template <int U, bool NT>
+__global__ void k_wgchunk(const u32x4* src, size_t n16, size_t chunk16, unsigned* sink) {
+  const unsigned lane = threadIdx.x & 63, w = threadIdx.x >> 6, W = blockDim.x >> 6;
+  u32x4 acc = {0, 0, 0, 0};
+  const size_t nchunks = n16 / chunk16;
+  for (size_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const u32x4* p = src + c * chunk16 + lane + 64 * w;
+    for (size_t r = 0; r < chunk16; r += size_t(64) * W * U) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ld<U, NT>(p + r + size_t(64) * W * u);
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc ^= v[u];
+    }
+  }
+  unsigned a = acc.x ^ acc.y ^ acc.z ^ acc.w;
+  if (a == 0x12345678u) atomicXor(sink, a);
+}
+
+template <typename F>
+double timeit(F f, int reps, double bytes) {
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  f();
+  CHECK(hipDeviceSynchronize());
+  std::vector<float> ts;
+  for (int i = 0; i < reps; ++i) {
+    CHECK(hipEventRecord(a));
+    f();
+    CHECK(hipEventRecord(b));
+    CHECK(hipEventSynchronize(b));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    ts.push_back(ms);
+  }
+  std::sort(ts.begin(), ts.end());
+  return bytes / (ts[ts.size() / 2] * 1e-3) / 1e9;
+}
+
+int main(int argc, char** argv) {
+  const double gib = argc > 1 ? atof(argv[1]) : 32.0;
+  const size_t bytes = size_t(gib * (1ull << 30));
+  const size_t n16 = bytes / 16;
+  u32x4* buf;
+  unsigned* sink;
+  CHECK(hipMalloc(&buf, bytes));
+  CHECK(hipMalloc(&sink, 4));
+  CHECK(hipMemset(buf, 0x5a, bytes));
+  int cus = 0;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const int reps = 5;
+  printf("buffer %.1f GiB, %d CUs\n", gib, cus);
+#define GS(U, NT, BLK, WGPERCU)                                                                          \
+  printf("gridstride U=%d nt=%d blk=%d wg/cu=%d : %.1f GB/s\n", U, NT, BLK, WGPERCU,                   \
+         timeit([&] { k_gridstride<U, NT><<<cus * WGPERCU, BLK>>>(buf, n16, sink); }, reps, double(bytes)))
+  GS(4, false, 256, 8);
+  GS(8, false, 256, 8);
+  GS(4, true, 256, 8);
+  GS(8, true, 256, 8);
+  GS(4, false, 1024, 2);
+  GS(4, false, 256, 16);
+  GS(2, false, 256, 32);
+#define WC(U, NT, BLK, WGPERCU, CH)                                                                      \
+  printf("wavechunk U=%d nt=%d blk=%d wg/cu=%d chunk=%zu KiB : %.1f GB/s\n", U, NT, BLK, WGPERCU,     \
+         size_t(CH) / 1024,                                                                            \
+         timeit([&] { k_wavechunk<U, NT><<<cus * WGPERCU, BLK>>>(buf, n16, size_t(CH) / 16, sink); }, reps, \
+                double(bytes)))
+  WC(4, false, 1024, 1, 1 << 20);
+  WC(8, false, 1024, 1, 1 << 20);
+  WC(4, true, 1024, 1, 1 << 20);
+  WC(8, true, 1024, 1, 1 << 20);
+  WC(4, false, 1024, 1, 256 << 10);
+  WC(4, false, 1024, 1, 64 << 10);
+  WC(4, false, 1024, 1, 4 << 20);
+  WC(4, false, 512, 2, 1 << 20);
+  WC(8, false, 512, 1, 1 << 20);
+  WC(16, false, 512, 1, 1 << 20);
+  WC(4, false, 256, 8, 1 << 20);
+#define WG(U, NT, BLK, WGPERCU, CH)                                                                       \
+  printf("wgchunk U=%d nt=%d blk=%d wg/cu=%d chunk=%zu KiB : %.1f GB/s\n", U, NT, BLK, WGPERCU,        \
+         size_t(CH) / 1024,                                                                              \
+         timeit([&] { k_wgchunk<U, NT><<<cus * WGPERCU, BLK>>>(buf, n16, size_t(CH) / 16, sink); }, reps, \
+                double(bytes)))
+  WG(4, false, 1024, 1, 1 << 20);
+  WG(2, false, 1024, 1, 1 << 20);
+  WG(4, true, 1024, 1, 1 << 20);
+  WG(4, false, 1024, 1, 16 << 20);
+  WG(4, false, 256, 4, 1 << 20);
+  WG(8, false, 256, 4, 1 << 20);
+  return 0;
+}

@@ -63,7 +63,7 @@ def test_sweep_every_offset_and_length(ctx, golden, piece, dynamic):
         assert np.array_equal(run(ctx, d, off, ln, max_len=max_len), exp0)
         assert np.array_equal(run(ctx, d, off, ln, init, max_len=max_len), expi)
     ctx.set_piece_bytes(256 * 1024)
-    ctx.set_schedule(True)
+    ctx.set_schedule(None)
 
 
 @pytest.mark.parametrize("piece", [256 * 1024, 4096, 1024, 1 << 20])
@@ -149,7 +149,7 @@ def test_cfg4_ragged_sample_vs_oracle(ctx, oracle):
             ctx.set_schedule(dyn)
             assert np.array_equal(run(ctx, d, off, ln), exp), (piece, dyn)
     ctx.set_piece_bytes(256 * 1024)
-    ctx.set_schedule(True)
+    ctx.set_schedule(None)
 
 
 def test_random_blocks_many_pieces_vs_oracle(ctx, oracle):
