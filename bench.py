@@ -28,6 +28,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import kvsep  # noqa: E402
+from kvsep import shard  # noqa: E402
 from kvsep import workloads as W  # noqa: E402
 
 GIB = float(1 << 30)
@@ -150,7 +151,7 @@ def main():
     # synthetic data, generated in HBM: rank r holds bytes [r*span, (r+1)*span) of one stream
     data = torch.empty(span + 64, dtype=torch.uint8, device=dev)
     seed = W.SEED + (1 if args.config.startswith("3") else 2 if args.config == "4" else 0)
-    kvsep.fill_splitmix64(data.data_ptr(), span, seed, rank * span)
+    kvsep.fill_splitmix64(data.data_ptr(), span, seed, shard.stream_offset(rank, span))
     d_off, d_len = to_dev_u64(off, dev), to_dev_u64(ln, dev)
     out = torch.zeros(count, dtype=torch.int32, device=dev)
     ctx.reserve(count, useful)
@@ -177,10 +178,7 @@ def main():
     elapsed = time.perf_counter() - t0
     ctx.set_timing(False)
     kern_ms, launches = ctx.get_timing()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = shard.max_over_ranks(elapsed, dist if world > 1 else None, dev)
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * useful * args.steps / GIB / elapsed
     kern_avg_ms = kern_ms / max(1, launches)
@@ -188,13 +186,8 @@ def main():
 
     # ---- outside the timed region: result digest gather (RCCL), parity spot check, ceilings
     crcs = out.cpu().numpy().view(np.uint32)
-    digest = kvsep.extend_host(0, crcs.tobytes())
-    digests = [digest]
-    if world > 1:
-        dt_ = torch.tensor([digest], dtype=torch.int64, device=dev)
-        gl = [torch.zeros_like(dt_) for _ in range(world)]
-        dist.all_gather(gl, dt_)
-        digests = [int(x.item()) for x in gl]
+    digest = shard.crc_of_crcs(crcs, kvsep.extend_host)
+    digests = shard.gather_digests(digest, dist if world > 1 else None, dev)
 
     sink = torch.zeros(4, dtype=torch.int32, device=dev)
     ctx.stream_read(data.data_ptr(), span, sink, stream=stream)  # warm

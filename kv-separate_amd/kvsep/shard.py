@@ -1,0 +1,67 @@
+"""Multi-GPU sharding of a CRC batch: blocks are independent, so each rank checksums
+its own shard from its own HBM and only 8-byte digests / timings cross the interconnect.
+
+Weak scaling: every rank holds the same block layout over its own slice of one global splitmix64
+stream -- rank r's byte j is global stream byte r*span + j -- so the N-GPU job equals one logical
+batch of N*count blocks.  Used by bench.py on RCCL and by tests/test_multiprocess_cpu.py on gloo.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def stream_offset(rank: int, span: int) -> int:
+    """Global stream position of rank `rank`'s first data byte."""
+    return rank * span
+
+
+def global_layout(off: np.ndarray, length: np.ndarray, span: int, world: int):
+    """The single logical batch the world checksums (for checking a sharded run)."""
+    off = np.asarray(off, dtype=np.uint64)
+    length = np.asarray(length, dtype=np.uint64)
+    offs = np.concatenate([off + np.uint64(stream_offset(r, span)) for r in range(world)])
+    return offs, np.tile(length, world)
+
+
+def crc_of_crcs(crcs: np.ndarray, extend_host) -> int:
+    """Size-independent digest of a result vector: CRC-32C over the little-endian u32 results."""
+    a = np.ascontiguousarray(crcs, dtype="<u4")
+    return int(extend_host(0, a.tobytes()))
+
+
+def max_over_ranks(value: float, dist, device) -> float:
+    import torch
+
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_digests(digest: int, dist, device) -> list[int]:
+    """All-gather one 32-bit digest per rank (the only result traffic between GPUs)."""
+    import torch
+
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return [digest]
+    t = torch.tensor([digest], dtype=torch.int64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [int(x.item()) for x in out]
+
+
+def reduce_verify(nbad: int, first_bad: int, dist, device) -> tuple[int, int]:
+    """Verify mode across ranks: total mismatches and the lowest mismatching GLOBAL block index
+    (first_bad already offset by rank*count; UINT64_MAX-as-int64 == -1 means none)."""
+    import torch
+
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return nbad, first_bad
+    big = np.iinfo(np.int64).max
+    n = torch.tensor([nbad], dtype=torch.int64, device=device)
+    f = torch.tensor([big if first_bad < 0 else first_bad], dtype=torch.int64, device=device)
+    dist.all_reduce(n, op=dist.ReduceOp.SUM)
+    dist.all_reduce(f, op=dist.ReduceOp.MIN)
+    fb = int(f.item())
+    return int(n.item()), (-1 if fb == big else fb)

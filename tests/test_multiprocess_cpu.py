@@ -1,0 +1,84 @@
+"""World-size-2 `gloo` rehearsal of the multi-GPU path (bench.py / kvsep.shard) on CPU: each rank
+checksums its own shard (host SSE4.2 leg of the library stands in for the kernel), ranks exchange only
+digests / timings / verify counts, and the result equals one logical batch checked by the oracle."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+
+COUNT, LEN = 64, 3000 + 5  # ragged-ish, odd lengths
+STRIDE = LEN + 8           # vlog-like framing gap
+SPAN = COUNT * STRIDE
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, os.path.join(ROOT, "kv-separate_amd"))
+    import kvsep
+    from kvsep import shard, splitmix64_bytes
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cpu")
+    off = np.arange(COUNT, dtype=np.uint64) * STRIDE + 8
+    ln = np.full(COUNT, LEN, dtype=np.uint64)
+    data = splitmix64_bytes(SPAN + 16, 0xC0FFEE, shard.stream_offset(rank, SPAN))
+    crcs = np.array([kvsep.extend_host(0, data[int(o):int(o + l)]) for o, l in zip(off, ln)], dtype=np.uint32)
+    digests = shard.gather_digests(shard.crc_of_crcs(crcs, kvsep.extend_host), dist, dev)
+    elapsed = shard.max_over_ranks(0.5 + rank, dist, dev)
+    # verify mode: rank 1 sees a corrupted record 7 (global index COUNT + 7)
+    expected = np.array([kvsep.mask(int(c)) for c in crcs], np.uint32)
+    if rank == 1:
+        expected[7] ^= 1
+    bad = np.nonzero(np.array([kvsep.mask(int(c)) for c in crcs], np.uint32) != expected)[0]
+    fb = int(bad[0]) + rank * COUNT if bad.size else -1
+    nbad, first = shard.reduce_verify(int(bad.size), fb, dist, dev)
+    q.put((rank, digests, elapsed, nbad, first, crcs.tolist()))
+    dist.destroy_process_group()
+
+
+def test_two_rank_shards_equal_one_logical_batch(oracle):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    sys.path.insert(0, os.path.join(ROOT, "kv-separate_amd"))
+    import kvsep
+    from kvsep import shard, splitmix64_bytes
+
+    # every rank sees the same gathered digests and the max elapsed
+    assert res[0][1] == res[1][1]
+    assert res[0][2] == res[1][2] == 1.5
+    assert res[0][3] == res[1][3] == 1 and res[0][4] == res[1][4] == COUNT + 7
+    # the sharded job equals one logical batch, checked by the oracle
+    off = np.arange(COUNT, dtype=np.uint64) * STRIDE + 8
+    goff, gln = shard.global_layout(off, np.full(COUNT, LEN, np.uint64), SPAN, world)
+    gdata = splitmix64_bytes(world * SPAN + 16, 0xC0FFEE, 0)
+    exp = oracle.batch(gdata, goff, gln, threads=2)
+    got = np.array(res[0][5] + res[1][5], dtype=np.uint32)
+    assert np.array_equal(got, exp)
+    assert res[0][1] == [shard.crc_of_crcs(exp[:COUNT], kvsep.extend_host),
+                         shard.crc_of_crcs(exp[COUNT:], kvsep.extend_host)]
