@@ -75,8 +75,17 @@ struct PiecesArgs {
   uint32_t* work_counter;           // dynamic schedule
   uint64_t piece_bytes;
   uint64_t max_pieces;              // capacity of pblk/partial
+  uint32_t static_contig;           // static schedule: contiguous item ranges per wave (else round-robin)
   const DevTables* tabs;
 };
+
+// Descriptor reads through the constant address space: wave-uniform indices then lower to scalar
+// s_load (lgkmcnt), so fetching the next item's descriptors never drains the vmcnt of in-flight
+// payload loads.  Descriptors are read-only for the whole launch.
+template <typename T>
+__device__ __forceinline__ T ldc(const T* p, uint64_t i) {
+  return reinterpret_cast<const __attribute__((address_space(4))) T*>(reinterpret_cast<uintptr_t>(p))[i];
+}
 
 __device__ __forceinline__ uint32_t lds_u32(const uint8_t* lds, uint32_t byte_off) {
   return *reinterpret_cast<const uint32_t*>(lds + byte_off);
@@ -137,46 +146,64 @@ __device__ __forceinline__ uint4 ld16(uintptr_t addr) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-// Raw CRC register after consuming [ps, pe) starting from register `reg` (no final inversion).
-// kG rows are computed while the next kG rows are in flight.
+// A work item's loads, issued ahead of its compute so a wave can overlap the next item's HBM latency
+// with the current item's serial lane merge.  All fields are wave-uniform except the vectors.
+template <int kG>
+struct Staged {
+  uintptr_t ps, pe, hbase, h0, a1, seg;
+  uint64_t K;     // body rows (0 = no body); the last row ends at a1
+  uint4 hc, tc;   // aligned 16 B around the head / the tail
+  uint4 v;        // row 0; lanes with v_ok == false (front mask) use zeros instead
+  uint4 A[kG];    // rows 1 .. kG (clamped to the last row)
+  bool v_ok;
+};
+
+// Issues a FIXED set of 3 + kG loads whatever the geometry (unneeded ones read `dummy`, a valid
+// device address), so the compiler can wait for exactly this item's loads with a counted vmcnt
+// while the next item's loads stay in flight; masking is deferred to finish().
 template <int kG, bool kNT>
-__device__ __forceinline__ uint32_t crc_piece(const uint8_t* lds, uintptr_t ps, uintptr_t pe, uint32_t reg,
-                                              uint32_t lane, uint32_t lc0, uint32_t lc1) {
-  const uintptr_t hbase = ps & ~uintptr_t(15);
-  uintptr_t h0 = (ps + 15) & ~uintptr_t(15);
-  if (h0 > pe) h0 = pe;
-  uintptr_t a1 = pe & ~uintptr_t(15);
-  if (a1 < h0) a1 = h0;
-
-  uint4 hc = make_uint4(0, 0, 0, 0), tc = make_uint4(0, 0, 0, 0);
-  if (ps < h0) hc = ld16(hbase);  // the aligned 16 B holding the head (never crosses a page)
-  if (a1 < pe) tc = ld16(a1);     // the aligned 16 B holding the tail
-
-  if (a1 > h0) {
-    const uint64_t K = (uint64_t(a1 - h0) + kRowBytes - 1) / kRowBytes;  // rows, the last ends at a1
-    const uintptr_t rb = a1 - K * kRowBytes;
-    const uintptr_t seg = rb + uintptr_t(lane) * 16u;
-    // issue the first rows' loads before the serial head work
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (seg >= h0) v = ld16<kNT>(seg);  // row 0 is front-masked: lanes before h0 hold zeros
-    // A holds rows r .. r+kG-1 (clamped to the last row); all issued before any compute, so a short
-    // piece (a 4 KiB block has 3 rows after row 0) has every row in flight at once.
-    const uint64_t last = K - 1;
-    uint4 A[kG];
-    if (K > 1) {
+__device__ __forceinline__ void stage(Staged<kG>& s, uintptr_t ps, uintptr_t pe, uint32_t lane, uintptr_t dummy) {
+  s.ps = ps;
+  s.pe = pe;
+  s.hbase = ps & ~uintptr_t(15);
+  s.h0 = (ps + 15) & ~uintptr_t(15);
+  if (s.h0 > pe) s.h0 = pe;
+  s.a1 = pe & ~uintptr_t(15);
+  if (s.a1 < s.h0) s.a1 = s.h0;
+  s.K = s.a1 > s.h0 ? (uint64_t(s.a1 - s.h0) + kRowBytes - 1) / kRowBytes : 0;
+  s.seg = s.a1 - s.K * kRowBytes + uintptr_t(lane) * 16u;
+  s.v_ok = s.K && s.seg >= s.h0;  // row 0 is front-masked: lanes before h0 hold zeros
+  s.hc = ld16(ps < s.h0 ? s.hbase : dummy);   // aligned 16 B holding the head (never crosses a page)
+  s.tc = ld16(s.a1 < pe ? s.a1 : dummy);      // aligned 16 B holding the tail
+  s.v = ld16<kNT>(s.v_ok ? s.seg : dummy);
+  const uint64_t last = s.K > 1 ? s.K - 1 : 0;
 #pragma unroll
-      for (int i = 0; i < kG; ++i) A[i] = ld16<kNT>(seg + (1 + i < last ? 1 + i : last) * kRowBytes);
-    }
-    if (ps < h0) reg = serial16(lds, reg, hc, int(ps - hbase), int(h0 - hbase));
-    if (seg == h0) v.x ^= reg;  // the head register enters as pending word at h0
+  for (int i = 0; i < kG; ++i)
+    s.A[i] = ld16<kNT>(last ? s.seg + (1 + i < last ? 1 + i : last) * kRowBytes : dummy);
+}
+
+// Raw CRC register after consuming the staged item [ps, pe) from register `reg` (no final inversion).
+// Rows beyond the staged ones stream kG at a time, the next kG in flight during compute.
+template <int kG, bool kNT, int kAbl = 0>  // kAbl != 0: diagnostic ablations (wrong results)
+__device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, uint32_t reg, uint32_t lane,
+                                           uint32_t lc0, uint32_t lc1) {
+  if (s.K) {
+    const uint64_t K = s.K, last = K - 1;
+    if (s.ps < s.h0) reg = serial16(lds, reg, s.hc, int(s.ps - s.hbase), int(s.h0 - s.hbase));
+    uint4 v = s.v_ok ? s.v : make_uint4(0, 0, 0, 0);
+    if (s.seg == s.h0) v.x ^= reg;  // the head register enters as pending word at h0
     uint32_t c0 = v.x, c1 = v.y, c2 = v.z, c3 = v.w;
 
 #define KVSEP_ROW(V)                                  \
   do {                                                \
+    if (kAbl == 2) {                                  \
+      c0 ^= (V).x; c1 ^= (V).y; c2 ^= (V).z; c3 ^= (V).w; \
+    } else {                                          \
     c0 = (V).x ^ fold1024(lds, c0, lc0, lc1);         \
     c1 = (V).y ^ fold1024(lds, c1, lc0, lc1);         \
     c2 = (V).z ^ fold1024(lds, c2, lc0, lc1);         \
     c3 = (V).w ^ fold1024(lds, c3, lc0, lc1);         \
+    }                                                 \
   } while (0)
 
     uint64_t r = 1;
@@ -184,16 +211,17 @@ __device__ __forceinline__ uint32_t crc_piece(const uint8_t* lds, uintptr_t ps, 
       uint4 B[kG];
       const uint64_t nr = r + kG;
 #pragma unroll
-      for (int i = 0; i < kG; ++i) B[i] = ld16<kNT>(seg + (nr + i < last ? nr + i : last) * kRowBytes);
+      for (int i = 0; i < kG; ++i) B[i] = ld16<kNT>(s.seg + (nr + i < last ? nr + i : last) * kRowBytes);
 #pragma unroll
-      for (int i = 0; i < kG; ++i) KVSEP_ROW(A[i]);
+      for (int i = 0; i < kG; ++i) KVSEP_ROW(s.A[i]);
 #pragma unroll
-      for (int i = 0; i < kG; ++i) A[i] = B[i];
+      for (int i = 0; i < kG; ++i) s.A[i] = B[i];
     }
 #pragma unroll
     for (int i = 0; i < kG; ++i)  // remainder rows r .. K-1, already in A
-      if (r + i < K) KVSEP_ROW(A[i]);
+      if (r + i < K) KVSEP_ROW(s.A[i]);
 #undef KVSEP_ROW
+    if (kAbl == 1) return c0 ^ c1 ^ c2 ^ c3 ^ lane;
     // lane merge: pending word at (16*lane + 12) of the last row
     uint32_t p = zmap(lds, kZ4Off, c0) ^ c1;
     p = zmap(lds, kZ4Off, p) ^ c2;
@@ -207,10 +235,10 @@ __device__ __forceinline__ uint32_t crc_piece(const uint8_t* lds, uintptr_t ps, 
     }
     p = __shfl(p, 63);               // pending word at a1 - 4
     reg = zmap(lds, kZ4Off, p);      // register at a1
-  } else if (ps < h0) {
-    reg = serial16(lds, reg, hc, int(ps - hbase), int(h0 - hbase));
+  } else if (s.ps < s.h0) {
+    reg = serial16(lds, reg, s.hc, int(s.ps - s.hbase), int(s.h0 - s.hbase));
   }
-  if (a1 < pe) reg = serial16(lds, reg, tc, 0, int(pe - a1));
+  if (s.a1 < s.pe) reg = serial16(lds, reg, s.tc, 0, int(s.pe - s.a1));
   return reg;
 }
 
@@ -224,7 +252,7 @@ __device__ __forceinline__ void emit_block(const PiecesArgs& a, uint64_t b, uint
   }
 }
 
-template <bool kPlanned, bool kDynamic, int kG, bool kNT>
+template <bool kPlanned, bool kDynamic, int kG, bool kNT, bool kAhead, int kAbl = 0>
 __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   const uint32_t tid = threadIdx.x;
@@ -251,16 +279,20 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
 
   uint64_t total = a.count;
   if (kPlanned) {
-    total = a.pstart[a.count];
+    total = ldc(a.pstart, a.count);
     if (total > a.max_pieces) total = a.max_pieces;  // scratch overflow guard (caller bound violated)
   }
 
   // Work distribution.  Static: wave w takes items w, w + nwaves, ...  Dynamic ("guided"): a wave
   // grabs a run of max(1, remaining / (4 * nwaves)) consecutive items with ONE atomic, so early
   // grabs are long and the tail is single items -- far below the ~88 dequeues/us one counter serves.
-  uint64_t lo, hi;
+  uint64_t lo = ~uint64_t(0), hi = 0, g = 0;
   uint64_t seen = 0;  // dynamic: counter value this wave last observed
-  auto grab = [&](uint64_t& l, uint64_t& h) {
+  auto next = [&]() -> bool {  // advance g to this wave's next work item
+    if (g + 1 < hi) {
+      ++g;
+      return true;
+    }
     if (kDynamic) {
       const uint64_t rem = total > seen ? total - seen : 0;
       uint64_t c = rem / (4 * nwaves);
@@ -268,46 +300,73 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
       if (c > 0xffffffffull) c = 0xffffffffull;
       uint32_t t = 0;
       if (lane == 0) t = atomicAdd(a.work_counter, uint32_t(c));
-      l = __builtin_amdgcn_readfirstlane(t);
-      h = l + c < total ? l + c : total;
-      seen = l + c;
+      lo = __builtin_amdgcn_readfirstlane(t);
+      hi = lo + c < total ? lo + c : total;
+      seen = lo + c;
+    } else if (a.static_contig) {  // wave w owns items [w*per, (w+1)*per): long per-wave streams
+      if (lo != ~uint64_t(0)) return false;
+      const uint64_t per = (total + nwaves - 1) / nwaves;
+      lo = (uint64_t(blockIdx.x) * kWavesPerWg + wave) * per;
+      hi = lo + per < total ? lo + per : total;
     } else {
-      l = (l == ~uint64_t(0)) ? uint64_t(blockIdx.x) * kWavesPerWg + wave : l + nwaves;
-      h = l + 1;
+      lo = (lo == ~uint64_t(0)) ? uint64_t(blockIdx.x) * kWavesPerWg + wave : lo + nwaves;
+      hi = lo + 1;
     }
+    g = lo;
+    return lo < total;
   };
-  lo = ~uint64_t(0);
-  grab(lo, hi);
-  while (lo < total) {
-    for (uint64_t g = lo; g < hi; ++g) {
-      uint64_t b;
-      uint64_t rs, re;
-      bool first, only;
-      if (kPlanned) {
-        b = a.pblk[g];
-        const uint64_t s0 = a.pstart[b], k = uint64_t(a.pstart[b + 1]) - s0, j = g - s0;
-        const uint64_t n = a.len[b];
-        re = n - (k - 1 - j) * a.piece_bytes;
-        rs = j ? n - (k - j) * a.piece_bytes : 0;
-        first = (j == 0);
-        only = (k == 1);
-      } else {
-        b = g;
-        rs = 0;
-        re = a.len[b];
-        first = true;
-        only = true;
-      }
-      const uintptr_t blk = reinterpret_cast<uintptr_t>(a.base) + a.off[b];
-      uint32_t reg0 = 0;
-      if (first) reg0 = ~(a.init ? a.init[b] : 0u);
-      const uint32_t reg = crc_piece<kG, kNT>(lds, blk + rs, blk + re, reg0, lane, lc0, lc1);
-      if (lane == 0) {
-        if (only) emit_block(a, b, ~reg);
-        else a.partial[g] = reg;
-      }
+  struct Item {
+    uint64_t g, b;
+    uint32_t reg0;
+    bool only;
+  };
+  auto resolve = [&](Item& it, Staged<kG>& st) {  // descriptors -> byte range, then issue its loads
+    uint64_t b, rs, re;
+    bool first;
+    it.g = g;
+    if (kPlanned) {
+      b = ldc(a.pblk, g);
+      const uint64_t s0 = ldc(a.pstart, b), k = uint64_t(ldc(a.pstart, b + 1)) - s0, j = g - s0;
+      const uint64_t n = ldc(a.len, b);
+      re = n - (k - 1 - j) * a.piece_bytes;
+      rs = j ? n - (k - j) * a.piece_bytes : 0;
+      first = (j == 0);
+      it.only = (k == 1);
+    } else {
+      b = g;
+      rs = 0;
+      re = ldc(a.len, b);
+      first = true;
+      it.only = true;
     }
-    grab(lo, hi);
+    it.b = b;
+    it.reg0 = first ? ~(a.init ? ldc(a.init, b) : 0u) : 0u;
+    const uintptr_t blk = reinterpret_cast<uintptr_t>(a.base) + ldc(a.off, b);
+    stage<kG, kNT>(st, blk + rs, blk + re, lane, reinterpret_cast<uintptr_t>(a.tabs));
+  };
+
+  Item cur, nxt;
+  Staged<kG> S, T;
+  bool have = next();
+  if (have) resolve(cur, S);
+  while (have) {
+    bool hn = false;
+    if (kAhead) {  // the next item's HBM loads overlap this item's compute
+      hn = next();
+      if (hn) resolve(nxt, T);
+    }
+    const uint32_t reg = finish<kG, kNT, kAbl>(lds, S, cur.reg0, lane, lc0, lc1);
+    if (lane == 0) {
+      if (cur.only) emit_block(a, cur.b, ~reg);
+      else a.partial[cur.g] = reg;
+    }
+    if (!kAhead) {
+      hn = next();
+      if (hn) resolve(nxt, T);
+    }
+    cur = nxt;
+    S = T;
+    have = hn;
   }
 }
 
@@ -407,6 +466,7 @@ struct kvsep_crc32c_ctx {
   uint64_t piece_bytes = 256 * 1024;
   int dynamic = -1;  // -1 auto, 0 static, 1 guided
   int variant = 1;   // rows per prefetch group / load policy, see launch_pieces
+  uint32_t static_contig = 1;
   // scratch
   uint64_t cap_count = 0, cap_pieces = 0;
   uint32_t* d_counts = nullptr;
@@ -499,11 +559,15 @@ hipEvent_t take_event(kvsep_crc32c_ctx* c) {
 
 template <bool P, bool D>
 void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs& a) {
-  switch (variant) {  // 0: 4 rows, plain loads  1: 4 rows, non-temporal  2: 8 rows, non-temporal  3: 8 rows plain
-    case 0: crc32c_pieces_kernel<P, D, 4, false><<<grid, kWgThreads, 0, s>>>(a); break;
-    case 1: crc32c_pieces_kernel<P, D, 4, true><<<grid, kWgThreads, 0, s>>>(a); break;
-    case 3: crc32c_pieces_kernel<P, D, 8, false><<<grid, kWgThreads, 0, s>>>(a); break;
-    default: crc32c_pieces_kernel<P, D, 8, true><<<grid, kWgThreads, 0, s>>>(a); break;
+  // 0: 4-row groups, plain loads   1: 4-row groups, non-temporal loads, next item staged ahead
+  // 2: as 1 without staging ahead   3: 8-row groups, non-temporal, staged ahead
+  switch (variant) {
+    case 0: crc32c_pieces_kernel<P, D, 4, false, true><<<grid, kWgThreads, 0, s>>>(a); break;
+    case 2: crc32c_pieces_kernel<P, D, 4, true, false><<<grid, kWgThreads, 0, s>>>(a); break;
+    case 3: crc32c_pieces_kernel<P, D, 8, true, true><<<grid, kWgThreads, 0, s>>>(a); break;
+    case 8: crc32c_pieces_kernel<P, D, 4, true, true, 1><<<grid, kWgThreads, 0, s>>>(a); break;  // diag
+    case 9: crc32c_pieces_kernel<P, D, 4, true, true, 2><<<grid, kWgThreads, 0, s>>>(a); break;  // diag
+    default: crc32c_pieces_kernel<P, D, 4, true, true><<<grid, kWgThreads, 0, s>>>(a); break;
   }
 }
 
@@ -564,6 +628,7 @@ int launch_batch(kvsep_crc32c_ctx* c, hipStream_t s, const void* base, const uin
     a.max_pieces = count;
   }
   const bool dyn = c->dynamic < 0 ? planned : c->dynamic == 1;  // auto: guided when planned, else static
+  a.static_contig = c->static_contig;
   if (dyn) {
     if (!c->d_counter) KVSEP_HIP(hipMalloc(&c->d_counter, 16));
     a.work_counter = c->d_counter;
@@ -627,6 +692,7 @@ int kvsep_crc32c_ctx_create(int device, kvsep_crc32c_ctx** out) {
   c->device = device;
   c->num_cus = prop.multiProcessorCount;
   if (const char* v = std::getenv("KVSEP_CRC_VARIANT")) c->variant = std::atoi(v);
+  if (const char* v = std::getenv("KVSEP_CRC_STATIC_RR")) c->static_contig = std::atoi(v) ? 0 : 1;
   KVSEP_HIP(hipSetDevice(device));
   int rc = upload_tables(c);
   if (rc) {

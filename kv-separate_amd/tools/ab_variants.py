@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of kernel variants in ONE process (cdna_hip_programming.md §5.4 rule 24).
+
+usage: python ab_variants.py --variants 1,2 --configs 3a,2 --rounds 5 --steps 5
+Prints per (config, variant) the median / min kernel time and GB/s (kernel-only HIP events).
+"""
+import argparse
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import kvsep  # noqa: E402
+from kvsep import workloads as W  # noqa: E402
+
+
+def layout(cfg):
+    return {"3a": W.cfg3_layout, "3b": lambda: W.cfg3_layout(vlog=True), "2": W.cfg2_layout,
+            "4": W.cfg4_layout}[cfg]()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="1,2")
+    ap.add_argument("--configs", default="3a,2")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--piece-kib", type=int, default=0)
+    args = ap.parse_args()
+    variants = [int(v) for v in args.variants.split(",")]
+    ctxs = {}
+    for v in variants:
+        os.environ["KVSEP_CRC_VARIANT"] = str(v)
+        ctxs[v] = kvsep.Context(0)
+        if args.piece_kib:
+            ctxs[v].set_piece_bytes(args.piece_kib * 1024)
+    dev = torch.device("cuda:0")
+    for cfg in args.configs.split(","):
+        off, ln = layout(cfg)
+        span = int(off[-1] + ln[-1])
+        useful = int(ln.sum())
+        data = torch.empty(span + 64, dtype=torch.uint8, device=dev)
+        kvsep.fill_splitmix64(data.data_ptr(), span, 5, 0)
+        d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+        d_len = torch.from_numpy(ln.view(np.int64)).to(dev)
+        outs = {v: torch.zeros(off.size, dtype=torch.int32, device=dev) for v in variants}
+        res = {v: [] for v in variants}
+        for v in variants:
+            ctxs[v].reserve(off.size, useful)
+            ctxs[v].batch_device(data.data_ptr(), d_off, d_len, outs[v], total_bytes=useful, max_len=int(ln.max()))
+        torch.cuda.synchronize()
+        for _ in range(args.rounds):
+            for v in variants:
+                c = ctxs[v]
+                c.set_timing(True)
+                for _ in range(args.steps):
+                    c.batch_device(data.data_ptr(), d_off, d_len, outs[v], total_bytes=useful, max_len=int(ln.max()))
+                torch.cuda.synchronize()
+                c.set_timing(False)
+                ms, n = c.get_timing()
+                res[v].append(ms / n)
+        ref = outs[variants[0]].cpu()
+        for v in variants:
+            same = bool(torch.equal(outs[v].cpu(), ref))
+            med, mn = statistics.median(res[v]), min(res[v])
+            print(f"cfg {cfg:3s} variant {v}: median {med:.4f} ms ({useful / med / 1e6:.1f} GB/s)  "
+                  f"min {mn:.4f} ms ({useful / mn / 1e6:.1f} GB/s)  same_as_v{variants[0]}={same}", flush=True)
+        del data, d_off, d_len, outs
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -124,39 +124,26 @@ int main(int argc, char** argv) {
 #define GS(U, NT, BLK, WGPERCU)                                                                          \
   printf("gridstride U=%d nt=%d blk=%d wg/cu=%d : %.1f GB/s\n", U, NT, BLK, WGPERCU,                   \
          timeit([&] { k_gridstride<U, NT><<<cus * WGPERCU, BLK>>>(buf, n16, sink); }, reps, double(bytes)))
-  GS(4, false, 256, 8);
-  GS(8, false, 256, 8);
-  GS(4, true, 256, 8);
-  GS(8, true, 256, 8);
-  GS(4, false, 1024, 2);
-  GS(4, false, 256, 16);
-  GS(2, false, 256, 32);
 #define WC(U, NT, BLK, WGPERCU, CH)                                                                      \
   printf("wavechunk U=%d nt=%d blk=%d wg/cu=%d chunk=%zu KiB : %.1f GB/s\n", U, NT, BLK, WGPERCU,     \
          size_t(CH) / 1024,                                                                            \
          timeit([&] { k_wavechunk<U, NT><<<cus * WGPERCU, BLK>>>(buf, n16, size_t(CH) / 16, sink); }, reps, \
                 double(bytes)))
-  WC(4, false, 1024, 1, 1 << 20);
-  WC(8, false, 1024, 1, 1 << 20);
-  WC(4, true, 1024, 1, 1 << 20);
-  WC(8, true, 1024, 1, 1 << 20);
-  WC(4, false, 1024, 1, 256 << 10);
-  WC(4, false, 1024, 1, 64 << 10);
-  WC(4, false, 1024, 1, 4 << 20);
-  WC(4, false, 512, 2, 1 << 20);
-  WC(8, false, 512, 1, 1 << 20);
-  WC(16, false, 512, 1, 1 << 20);
-  WC(4, false, 256, 8, 1 << 20);
 #define WG(U, NT, BLK, WGPERCU, CH)                                                                       \
   printf("wgchunk U=%d nt=%d blk=%d wg/cu=%d chunk=%zu KiB : %.1f GB/s\n", U, NT, BLK, WGPERCU,        \
          size_t(CH) / 1024,                                                                              \
          timeit([&] { k_wgchunk<U, NT><<<cus * WGPERCU, BLK>>>(buf, n16, size_t(CH) / 16, sink); }, reps, \
                 double(bytes)))
-  WG(4, false, 1024, 1, 1 << 20);
-  WG(2, false, 1024, 1, 1 << 20);
-  WG(4, true, 1024, 1, 1 << 20);
-  WG(4, false, 1024, 1, 16 << 20);
-  WG(4, false, 256, 4, 1 << 20);
-  WG(8, false, 256, 4, 1 << 20);
+  WC(4, true, 1024, 1, 4 << 10);
+  WC(4, true, 1024, 1, 16 << 10);
+  WC(4, true, 1024, 1, 64 << 10);
+  WC(4, true, 1024, 1, 1 << 20);
+  WC(4, false, 1024, 1, 4 << 10);
+  WC(4, true, 256, 8, 4 << 10);
+  WC(4, true, 512, 4, 4 << 10);
+  WG(4, true, 1024, 1, 64 << 10);
+  WG(4, true, 1024, 1, 16 << 10);
+  WG(1, true, 1024, 1, 16 << 10);
+  GS(4, true, 256, 8);
   return 0;
 }
