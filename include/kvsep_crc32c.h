@@ -96,6 +96,37 @@ int kvsep_crc32c_batch_host_span(kvsep_crc32c_ctx* ctx, const char* host_base, u
                                  const uint64_t* off, const uint64_t* len, const uint32_t* init, uint32_t* out,
                                  uint64_t count);
 
+/* ---------------------------------------------------------------- framings (batched call sites)
+ * vlog records (db/value_log_writer.cc:46-76, db/value_log_reader.cc:86-138):
+ *   [Mask(Value(payload)) LE32][len LE32][payload], back to back from offset 0. */
+/* Header walk: fills off/len/stored (nullable) for up to `cap` complete records; returns the number of
+ * complete records; a truncated header or payload ends the walk (the reader's eof). */
+uint64_t kvsep_vlog_walk(const char* buf, uint64_t n, uint64_t* off, uint64_t* len, uint32_t* stored, uint64_t cap,
+                         uint64_t* consumed);
+/* Recovery / GC scan: walk + one batched GPU checksum + compare.  *ngood = records before the first checksum
+ * mismatch (the reader reports "checksum mismatch" there and stops), *good_bytes = end offset of the last good one. */
+int kvsep_vlog_verify_host(kvsep_crc32c_ctx* ctx, const char* buf, uint64_t n, uint64_t* nrecords, uint64_t* ngood,
+                           uint64_t* good_bytes);
+/* Group-commit write side: frames `count` payloads into dst (needs sum(8 + len) bytes, *written). */
+int kvsep_vlog_frame_host(kvsep_crc32c_ctx* ctx, const char* const* payload, const uint64_t* len, uint64_t count,
+                          char* dst, uint64_t dst_cap, uint64_t* written);
+/* log / MANIFEST physical records (db/log_reader.cc:189-272): 32 KiB blocks of [crc LE32][len LE16][type][payload],
+ * crc = Mask(Value(type || payload)).  Walk returns off = header + 6 (the type byte), len = 1 + payload length. */
+uint64_t kvsep_log_walk(const char* buf, uint64_t n, uint64_t* off, uint64_t* len, uint32_t* stored, uint8_t* type,
+                        uint64_t cap);
+int kvsep_log_verify_host(kvsep_crc32c_ctx* ctx, const char* buf, uint64_t n, uint8_t* ok, uint64_t cap,
+                          uint64_t* nrecords);
+/* SST block trailers (table/table_builder.cc:209-232): masked_out[i] = Mask(Extend(Value(block_i), &types[i], 1)),
+ * the LE32 word written after the type byte.  Device pointers, async on stream. */
+int kvsep_sst_trailers_device(kvsep_crc32c_ctx* ctx, void* stream, const void* base, const uint64_t* off,
+                              const uint64_t* len, const uint8_t* types, uint32_t* masked_out, uint64_t count,
+                              uint64_t total_bytes, uint64_t max_len);
+/* SST block read check (table/format.cc:99-106): the file image holds [block][type][trailer word]; out[i] =
+ * Value(block, len + 1) (= Unmask(stored) when intact); *first_bad / *nbad as in kvsep_crc32c_verify_device. */
+int kvsep_sst_verify_device(kvsep_crc32c_ctx* ctx, void* stream, const void* file_base, const uint64_t* off,
+                            const uint64_t* len, uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count,
+                            uint64_t total_bytes, uint64_t max_len);
+
 /* ---------------------------------------------------------------- support
  * Synthetic data: byte i of the stream is byte (i&7) of splitmix64 word (i>>3) of `seed`
  * (word j = mix(seed + (j+1)*0x9E3779B97F4A7C15)); writes bytes [stream_offset, +nbytes) to dst. */

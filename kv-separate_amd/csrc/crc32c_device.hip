@@ -395,6 +395,27 @@ __global__ void crc32c_plan_count_kernel(const uint64_t* len, uint64_t count, ui
   counts[b] = n <= piece_bytes ? 1u : uint32_t((n + piece_bytes - 1) / piece_bytes);
 }
 
+// SST write side (table/table_builder.cc:222-225): crc = Extend(Value(block), &type, 1); trailer word = Mask(crc).
+__global__ void sst_trailer_finish_kernel(const uint32_t* crc, const uint8_t* types, uint32_t* masked,
+                                          uint64_t count, const DevTables* tabs) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  uint32_t l = ~crc[i];
+  l = tabs->byte1[(l ^ types[i]) & 0xffu] ^ (l >> 8);  // one STEP1 (util/crc32c.cc:287-292)
+  masked[i] = mask_crc(~l);
+}
+
+// SST read side (table/format.cc:99-106): the block is followed by [type][Mask(crc) LE32] in the file
+// image, so the check is Value(data, n + 1) against the stored word.
+__global__ void sst_verify_prep_kernel(const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                                       uint64_t* len1, uint32_t* stored, uint64_t count) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const uint8_t* t = base + off[i] + len[i] + 1;
+  len1[i] = len[i] + 1;
+  stored[i] = uint32_t(t[0]) | (uint32_t(t[1]) << 8) | (uint32_t(t[2]) << 16) | (uint32_t(t[3]) << 24);
+}
+
 __global__ void crc32c_plan_expand_kernel(const uint32_t* pstart, uint64_t count, uint64_t max_pieces,
                                           uint32_t* pblk) {
   const uint64_t b = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -475,6 +496,9 @@ struct kvsep_crc32c_ctx {
   uint32_t* d_partial = nullptr;
   uint32_t* d_counter = nullptr;
   unsigned long long* d_verify_scratch = nullptr;  // [first_bad, nbad] when the caller passes none
+  uint64_t* d_sst_len1 = nullptr;   // SST verify scratch: len + 1 ...
+  uint32_t* d_sst_stored = nullptr; // ... and the stored trailer words
+  uint64_t cap_sst = 0;
   void* d_scan_tmp = nullptr;
   size_t scan_tmp_bytes = 0;
   // timing
@@ -711,6 +735,8 @@ void kvsep_crc32c_ctx_destroy(kvsep_crc32c_ctx* c) {
   hipFree(c->d_tabs);
   hipFree(c->d_counter);
   hipFree(c->d_verify_scratch);
+  hipFree(c->d_sst_len1);
+  hipFree(c->d_sst_stored);
   for (auto& p : c->ev_pending) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
   for (auto e : c->ev_pool) hipEventDestroy(e);
   release_staging(c->staging);
@@ -802,6 +828,48 @@ int kvsep_fill_splitmix64_device(void* stream, void* dst, uint64_t nbytes, uint6
   }
   KVSEP_HIP(hipGetLastError());
   return KVSEP_OK;
+}
+
+int kvsep_sst_trailers_device(kvsep_crc32c_ctx* c, void* stream, const void* base, const uint64_t* off,
+                              const uint64_t* len, const uint8_t* types, uint32_t* masked_out, uint64_t count,
+                              uint64_t total_bytes, uint64_t max_len) {
+  if (!c || !types || !masked_out) return set_err(KVSEP_EINVAL, "null argument");
+  std::lock_guard<std::mutex> g(c->mu);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int rc = launch_batch(c, s, base, off, len, nullptr, nullptr, masked_out, nullptr, nullptr, count, total_bytes,
+                        max_len);
+  if (rc || !count) return rc;
+  sst_trailer_finish_kernel<<<unsigned((count + 255) / 256), 256, 0, s>>>(masked_out, types, masked_out, count,
+                                                                          c->d_tabs);
+  KVSEP_HIP(hipGetLastError());
+  return KVSEP_OK;
+}
+
+int kvsep_sst_verify_device(kvsep_crc32c_ctx* c, void* stream, const void* file_base, const uint64_t* off,
+                            const uint64_t* len, uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count,
+                            uint64_t total_bytes, uint64_t max_len) {
+  if (!c || !file_base || !off || !len || !out) return set_err(KVSEP_EINVAL, "null argument");
+  std::lock_guard<std::mutex> g(c->mu);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  KVSEP_HIP(hipSetDevice(c->device));
+  if (count > c->cap_sst) {
+    KVSEP_HIP(hipStreamSynchronize(s));
+    hipFree(c->d_sst_len1);
+    hipFree(c->d_sst_stored);
+    c->d_sst_len1 = nullptr;
+    c->d_sst_stored = nullptr;
+    c->cap_sst = 0;
+    KVSEP_HIP(hipMalloc(&c->d_sst_len1, count * 8));
+    KVSEP_HIP(hipMalloc(&c->d_sst_stored, count * 4));
+    c->cap_sst = count;
+  }
+  if (count) {
+    sst_verify_prep_kernel<<<unsigned((count + 255) / 256), 256, 0, s>>>(static_cast<const uint8_t*>(file_base), off,
+                                                                        len, c->d_sst_len1, c->d_sst_stored, count);
+    KVSEP_HIP(hipGetLastError());
+  }
+  return launch_batch(c, s, file_base, off, c->d_sst_len1, nullptr, c->d_sst_stored, out, first_bad, nbad, count,
+                      total_bytes + count, max_len ? max_len + 1 : 0);
 }
 
 int kvsep_stream_read_device(kvsep_crc32c_ctx* c, void* stream, const void* src, uint64_t nbytes, uint32_t* sink) {

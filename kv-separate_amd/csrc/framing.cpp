@@ -1,0 +1,149 @@
+// framing.cpp -- the record/block framings that call crc32c in kv-separate, batched onto the engine.
+//
+//   vlog       db/value_log_writer.cc:46-76, db/value_log_reader.cc:86-138, db/log_format.h:40
+//              record = [Mask(Value(payload)) LE32][len LE32][payload]; the reader stops at the first
+//              truncated record (eof) and at the first checksum mismatch (ReportCorruption + eof_).
+//   log/MANIFEST db/log_writer.cc:84-115, db/log_reader.cc:189-272, db/log_format.h:16-33
+//              32 KiB blocks of [crc LE32][len LE16][type u8][payload]; crc = Mask(Value(type||payload));
+//              < 7 trailing bytes of a block are padding; type 0 with length 0 is preallocated space.
+//   SST block  table/table_builder.cc:209-232, table/format.cc:73-108, table/format.h:81
+//              block, then a 5-byte trailer [type u8][Mask(Extend(Value(block), &type, 1)) LE32].
+//
+// The serial parts (header walks) stay on the host; every checksum goes through one batched call.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../include/kvsep_crc32c.h"
+#include "kvsep_internal.h"
+
+namespace {
+
+inline uint32_t le32(const char* p) {
+  const auto* b = reinterpret_cast<const uint8_t*>(p);
+  return uint32_t(b[0]) | (uint32_t(b[1]) << 8) | (uint32_t(b[2]) << 16) | (uint32_t(b[3]) << 24);
+}
+
+inline void put_le32(char* p, uint32_t v) {
+  auto* b = reinterpret_cast<uint8_t*>(p);
+  b[0] = uint8_t(v);
+  b[1] = uint8_t(v >> 8);
+  b[2] = uint8_t(v >> 16);
+  b[3] = uint8_t(v >> 24);
+}
+
+constexpr uint64_t kVlogHeader = 8;       // db/log_format.h:40
+constexpr uint64_t kLogBlock = 32768;     // db/log_format.h:30
+constexpr uint64_t kLogHeader = 7;        // db/log_format.h:33
+
+}  // namespace
+
+extern "C" {
+
+uint64_t kvsep_vlog_walk(const char* buf, uint64_t n, uint64_t* off, uint64_t* len, uint32_t* stored,
+                         uint64_t cap, uint64_t* consumed) {
+  uint64_t p = 0, k = 0;
+  while (p + kVlogHeader <= n) {  // db/value_log_reader.cc:91-96: short header = eof
+    const uint64_t l = le32(buf + p + 4);
+    if (l > n - p - kVlogHeader) break;  // :107-108: short payload = eof
+    if (k < cap) {
+      if (off) off[k] = p + kVlogHeader;
+      if (len) len[k] = l;
+      if (stored) stored[k] = le32(buf + p);
+    }
+    ++k;
+    p += kVlogHeader + l;
+  }
+  if (consumed) *consumed = p;
+  return k;
+}
+
+int kvsep_vlog_verify_host(kvsep_crc32c_ctx* ctx, const char* buf, uint64_t n, uint64_t* nrecords, uint64_t* ngood,
+                           uint64_t* good_bytes) {
+  if (!ctx || (!buf && n)) return KVSEP_EINVAL;
+  const uint64_t cnt = kvsep_vlog_walk(buf, n, nullptr, nullptr, nullptr, 0, nullptr);
+  std::vector<uint64_t> off(cnt), len(cnt);
+  std::vector<uint32_t> stored(cnt), crc(cnt);
+  kvsep_vlog_walk(buf, n, off.data(), len.data(), stored.data(), cnt, nullptr);
+  if (cnt) {
+    const int rc = kvsep_crc32c_batch_host_span(ctx, buf, n, off.data(), len.data(), nullptr, crc.data(), cnt);
+    if (rc) return rc;
+  }
+  uint64_t g = 0;
+  while (g < cnt && kvsep_crc32c_mask(crc[g]) == stored[g]) ++g;  // :109-122: stop at first mismatch
+  if (nrecords) *nrecords = cnt;
+  if (ngood) *ngood = g;
+  if (good_bytes) *good_bytes = g ? off[g - 1] + len[g - 1] : 0;
+  return KVSEP_OK;
+}
+
+int kvsep_vlog_frame_host(kvsep_crc32c_ctx* ctx, const char* const* payload, const uint64_t* len, uint64_t count,
+                          char* dst, uint64_t dst_cap, uint64_t* written) {
+  if (!ctx || (count && (!payload || !len))) return KVSEP_EINVAL;
+  uint64_t need = 0;
+  for (uint64_t i = 0; i < count; ++i) {
+    if (len[i] > 0xffffffffull) return KVSEP_EINVAL;  // db/value_log_writer.cc:48 (LE32 length)
+    need += kVlogHeader + len[i];
+  }
+  if (written) *written = need;
+  if (need > dst_cap || (need && !dst)) return KVSEP_EINVAL;
+  std::vector<uint32_t> crc(count);
+  if (count) {
+    const int rc = kvsep_crc32c_batch_host(ctx, nullptr, payload, len, crc.data(), count);
+    if (rc) return rc;
+  }
+  uint64_t p = 0;
+  for (uint64_t i = 0; i < count; ++i) {  // db/value_log_writer.cc:57-70
+    put_le32(dst + p, kvsep_crc32c_mask(crc[i]));
+    put_le32(dst + p + 4, uint32_t(len[i]));
+    if (len[i]) std::memcpy(dst + p + kVlogHeader, payload[i], len[i]);
+    p += kVlogHeader + len[i];
+  }
+  return KVSEP_OK;
+}
+
+uint64_t kvsep_log_walk(const char* buf, uint64_t n, uint64_t* off, uint64_t* len, uint32_t* stored, uint8_t* type,
+                        uint64_t cap) {
+  uint64_t k = 0;
+  for (uint64_t blk = 0; blk < n; blk += kLogBlock) {
+    const uint64_t end = blk + kLogBlock < n ? blk + kLogBlock : n;
+    uint64_t p = blk;
+    while (end - p >= kLogHeader) {  // db/log_reader.cc:195-220: < 7 bytes left = block trailer
+      const uint8_t* h = reinterpret_cast<const uint8_t*>(buf + p);
+      const uint64_t l = uint64_t(h[4]) | (uint64_t(h[5]) << 8);
+      const uint8_t t = h[6];
+      if (kLogHeader + l > end - p) break;      // :229-241 bad record length: drop rest of block
+      if (t == 0 && l == 0) break;               // :243-249 preallocated zero region
+      if (k < cap) {
+        if (off) off[k] = p + 6;                 // CRC covers type || payload (:247-248)
+        if (len) len[k] = 1 + l;
+        if (stored) stored[k] = le32(buf + p);
+        if (type) type[k] = t;
+      }
+      ++k;
+      p += kLogHeader + l;
+    }
+  }
+  return k;
+}
+
+int kvsep_log_verify_host(kvsep_crc32c_ctx* ctx, const char* buf, uint64_t n, uint8_t* ok, uint64_t cap,
+                          uint64_t* nrecords) {
+  if (!ctx || (!buf && n)) return KVSEP_EINVAL;
+  const uint64_t cnt = kvsep_log_walk(buf, n, nullptr, nullptr, nullptr, nullptr, 0);
+  if (nrecords) *nrecords = cnt;
+  if (cnt > cap || (cnt && !ok)) return KVSEP_EINVAL;
+  std::vector<uint64_t> off(cnt), len(cnt);
+  std::vector<uint32_t> stored(cnt), crc(cnt);
+  kvsep_log_walk(buf, n, off.data(), len.data(), stored.data(), nullptr, cnt);
+  if (cnt) {
+    const int rc = kvsep_crc32c_batch_host_span(ctx, buf, n, off.data(), len.data(), nullptr, crc.data(), cnt);
+    if (rc) return rc;
+  }
+  for (uint64_t i = 0; i < cnt; ++i) ok[i] = crc[i] == kvsep_crc32c_unmask(stored[i]) ? 1 : 0;  // :250-258
+  return KVSEP_OK;
+}
+
+}  // extern "C"

@@ -75,6 +75,22 @@ _SIGS = {
                                                     ctypes.c_uint64]),
     "kvsep_stream_read_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                                 ctypes.c_void_p]),
+    "kvsep_vlog_walk": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+    "kvsep_vlog_verify_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p]),
+    "kvsep_vlog_frame_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+    "kvsep_log_walk": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
+    "kvsep_log_verify_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                             ctypes.c_uint64, ctypes.c_void_p]),
+    "kvsep_sst_trailers_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                 ctypes.c_uint64, ctypes.c_uint64]),
+    "kvsep_sst_verify_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]),
     "kvsep_last_error": (ctypes.c_char_p, []),
     "kvsep_build_info": (ctypes.c_char_p, []),
     "kvsep_device_count": (ctypes.c_int, []),
@@ -266,6 +282,84 @@ class Context:
         _check(lib().kvsep_crc32c_batch_host(self._h, ip, ptrs, lens.ctypes.data_as(ctypes.c_void_p),
                                              out.ctypes.data_as(ctypes.c_void_p), n), "kvsep_crc32c_batch_host")
         return out
+
+
+    # -- framings (vlog / log / SST call sites)
+    def vlog_verify(self, image):
+        """db/value_log_reader.cc:86-138 over a whole vlog image -> (records, good, good_bytes)."""
+        p, keep = _buf(image)
+        n, g, gb = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().kvsep_vlog_verify_host(self._h, p, keep.nbytes, ctypes.byref(n), ctypes.byref(g),
+                                            ctypes.byref(gb)), "kvsep_vlog_verify_host")
+        return n.value, g.value, gb.value
+
+    def vlog_frame(self, payloads):
+        """db/value_log_writer.cc:46-76 for a batch of payloads -> bytes of the framed records."""
+        keep = [_buf(b) for b in payloads]
+        k = len(payloads)
+        ptrs = (ctypes.c_void_p * max(k, 1))(*[x[0].value for x in keep])
+        lens = np.array([x[1].nbytes for x in keep], dtype=np.uint64)
+        need = int(lens.sum()) + 8 * k
+        dst = np.zeros(max(need, 1), dtype=np.uint8)
+        w = ctypes.c_uint64()
+        _check(lib().kvsep_vlog_frame_host(self._h, ptrs, lens.ctypes.data_as(ctypes.c_void_p), k,
+                                           dst.ctypes.data_as(ctypes.c_void_p), dst.nbytes, ctypes.byref(w)),
+               "kvsep_vlog_frame_host")
+        return dst[:w.value].tobytes()
+
+    def log_verify(self, image):
+        """db/log_reader.cc:246-259 per physical record of a log/MANIFEST image -> array of 0/1."""
+        p, keep = _buf(image)
+        cnt = log_walk(image)[0].size
+        ok = np.zeros(max(cnt, 1), dtype=np.uint8)
+        n = ctypes.c_uint64()
+        _check(lib().kvsep_log_verify_host(self._h, p, keep.nbytes, ok.ctypes.data_as(ctypes.c_void_p), ok.size,
+                                           ctypes.byref(n)), "kvsep_log_verify_host")
+        return ok[:n.value]
+
+    def sst_trailers_device(self, base, off, length, types, masked_out, count=None, total_bytes=None, max_len=0,
+                            stream=None):
+        count = int(off.numel()) if count is None else count
+        if total_bytes is None:
+            total_bytes = int(length.sum().item()) if count else 0
+        _check(lib().kvsep_sst_trailers_device(self._h, _stream_handle(stream), _dptr(base), _dptr(off),
+                                               _dptr(length), _dptr(types), _dptr(masked_out), count, total_bytes,
+                                               max_len), "kvsep_sst_trailers_device")
+
+    def sst_verify_device(self, file_base, off, length, out, first_bad, nbad, count=None, total_bytes=None,
+                          max_len=0, stream=None):
+        count = int(off.numel()) if count is None else count
+        if total_bytes is None:
+            total_bytes = int(length.sum().item()) if count else 0
+        _check(lib().kvsep_sst_verify_device(self._h, _stream_handle(stream), _dptr(file_base), _dptr(off),
+                                             _dptr(length), _dptr(out), _dptr(first_bad), _dptr(nbad), count,
+                                             total_bytes, max_len), "kvsep_sst_verify_device")
+
+
+def vlog_walk(image):
+    """Header walk of a vlog image (db/value_log_reader.cc:86-108) -> (off, len, stored, consumed)."""
+    p, keep = _buf(image)
+    cnt = lib().kvsep_vlog_walk(p, keep.nbytes, None, None, None, 0, None)
+    off = np.zeros(cnt, np.uint64)
+    ln = np.zeros(cnt, np.uint64)
+    st = np.zeros(cnt, np.uint32)
+    used = ctypes.c_uint64()
+    lib().kvsep_vlog_walk(p, keep.nbytes, off.ctypes.data_as(ctypes.c_void_p), ln.ctypes.data_as(ctypes.c_void_p),
+                          st.ctypes.data_as(ctypes.c_void_p), cnt, ctypes.byref(used))
+    return off, ln, st, used.value
+
+
+def log_walk(image):
+    """Physical-record walk of a log/MANIFEST image (db/log_reader.cc:189-272) -> (off, len, stored, type)."""
+    p, keep = _buf(image)
+    cnt = lib().kvsep_log_walk(p, keep.nbytes, None, None, None, None, 0)
+    off = np.zeros(cnt, np.uint64)
+    ln = np.zeros(cnt, np.uint64)
+    st = np.zeros(cnt, np.uint32)
+    ty = np.zeros(cnt, np.uint8)
+    lib().kvsep_log_walk(p, keep.nbytes, off.ctypes.data_as(ctypes.c_void_p), ln.ctypes.data_as(ctypes.c_void_p),
+                         st.ctypes.data_as(ctypes.c_void_p), ty.ctypes.data_as(ctypes.c_void_p), cnt)
+    return off, ln, st, ty
 
 
 def fill_splitmix64(dst, nbytes: int, seed: int, stream_offset: int = 0, stream=None):
