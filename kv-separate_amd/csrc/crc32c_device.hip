@@ -226,12 +226,15 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     uint32_t p = zmap(lds, kZ4Off, c0) ^ c1;
     p = zmap(lds, kZ4Off, p) ^ c2;
     p = zmap(lds, kZ4Off, p) ^ c3;
-    // butterfly over lanes: level j moves a 16*2^j-byte segment's pending word forward by 16*2^j
+    // reduction over lanes: at level j the lanes whose low j+1 bits are all ones (64 >> (j+1) of them)
+    // pull the pending word of the segment 16*2^j bytes before theirs and carry it forward by 16*2^j.
+    // Only those lanes touch LDS (exec-masked), which keeps the non-replicated tree tables' bank
+    // conflicts small -- the tree is the LDS hot spot for short blocks.
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const uint32_t o = __shfl_xor(p, 1 << j);
-      const uint32_t moved = zmap(lds, kTreeOff + 4096u * j, o) ^ p;
-      p = (lane & (1u << j)) ? moved : p;
+      const uint32_t m = (2u << j) - 1u;
+      if ((lane & m) == m) p = zmap(lds, kTreeOff + 4096u * j, o) ^ p;
     }
     p = __shfl(p, 63);               // pending word at a1 - 4
     reg = zmap(lds, kZ4Off, p);      // register at a1
@@ -258,16 +261,18 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
   const uint32_t tid = threadIdx.x;
   // ---- fill LDS: replicated Z_1024 (coalesced dword stores), then the small tables as one run
   {
-    uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
+    // 16-B stores: 4 consecutive dwords of the replicated image are 4 copies of one entry
+    uint4* l128 = reinterpret_cast<uint4*>(lds);
     const uint32_t* z = &a.tabs->z1024[0][0];
-#pragma unroll 4
-    for (uint32_t i = 0; i < 32; ++i) {
-      const uint32_t idx = tid + i * kWgThreads;  // dword index in the replicated image
-      const uint32_t pair = idx >> 14, b = (idx >> 6) & 255u, half = (idx >> 5) & 1u;
-      l32[idx] = z[(2u * pair + half) * 256u + b];
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) {
+      const uint32_t q = tid + i * kWgThreads;  // uint4 index in the replicated image
+      const uint32_t idx = q * 4, pair = idx >> 14, b = (idx >> 6) & 255u, half = (idx >> 5) & 1u;
+      const uint32_t v = z[(2u * pair + half) * 256u + b];
+      l128[q] = make_uint4(v, v, v, v);
     }
-    const uint32_t* src = &a.tabs->z4[0][0];
-    for (uint32_t i = tid; i < (kLdsBytes - kZ4Off) / 4; i += kWgThreads) l32[kZ4Off / 4 + i] = src[i];
+    const uint4* src = reinterpret_cast<const uint4*>(&a.tabs->z4[0][0]);
+    for (uint32_t i = tid; i < (kLdsBytes - kZ4Off) / 16; i += kWgThreads) l128[kZ4Off / 16 + i] = src[i];
   }
   __syncthreads();
 
@@ -283,16 +288,13 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
     if (total > a.max_pieces) total = a.max_pieces;  // scratch overflow guard (caller bound violated)
   }
 
-  // Work distribution.  Static: wave w takes items w, w + nwaves, ...  Dynamic ("guided"): a wave
-  // grabs a run of max(1, remaining / (4 * nwaves)) consecutive items with ONE atomic, so early
-  // grabs are long and the tail is single items -- far below the ~88 dequeues/us one counter serves.
-  uint64_t lo = ~uint64_t(0), hi = 0, g = 0;
+  // Work distribution.  Static: wave w owns the run [w*per, (w+1)*per) (or round-robin single items).
+  // Dynamic ("guided"): a wave grabs a run of max(1, remaining / (4 * nwaves)) consecutive items with
+  // ONE atomic, so early runs are long and the tail is single items -- far below the ~88 dequeues/us a
+  // single counter serves.
+  uint64_t lo = ~uint64_t(0), hi = 0;
   uint64_t seen = 0;  // dynamic: counter value this wave last observed
-  auto next = [&]() -> bool {  // advance g to this wave's next work item
-    if (g + 1 < hi) {
-      ++g;
-      return true;
-    }
+  auto grab = [&]() -> bool {
     if (kDynamic) {
       const uint64_t rem = total > seen ? total - seen : 0;
       uint64_t c = rem / (4 * nwaves);
@@ -300,10 +302,10 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
       if (c > 0xffffffffull) c = 0xffffffffull;
       uint32_t t = 0;
       if (lane == 0) t = atomicAdd(a.work_counter, uint32_t(c));
-      lo = __builtin_amdgcn_readfirstlane(t);
+      lo = uint32_t(__builtin_amdgcn_readfirstlane(t));
       hi = lo + c < total ? lo + c : total;
       seen = lo + c;
-    } else if (a.static_contig) {  // wave w owns items [w*per, (w+1)*per): long per-wave streams
+    } else if (a.static_contig) {
       if (lo != ~uint64_t(0)) return false;
       const uint64_t per = (total + nwaves - 1) / nwaves;
       lo = (uint64_t(blockIdx.x) * kWavesPerWg + wave) * per;
@@ -312,61 +314,86 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
       lo = (lo == ~uint64_t(0)) ? uint64_t(blockIdx.x) * kWavesPerWg + wave : lo + nwaves;
       hi = lo + 1;
     }
-    g = lo;
     return lo < total;
+  };
+
+  // Descriptor window: lane i resolves item w0 + i (block, byte range, initial register) with vector
+  // loads issued once per 64 items; items are then taken out with readlane.  Keeps dependent
+  // first-touch descriptor loads out of the per-item critical path (short blocks).
+  uint64_t w0 = 0, wn = 0;        // window [w0, w0 + wn) of the current run
+  uintptr_t w_ps = 0, w_pe = 0;   // per lane
+  uint32_t w_b = 0, w_reg0 = 0, w_only = 0;
+  auto fill = [&](uint64_t start, uint64_t stop) {
+    w0 = start;
+    wn = stop - start < 64 ? stop - start : 64;
+    const uint64_t g = start + lane;
+    w_ps = w_pe = 0;
+    w_b = w_reg0 = w_only = 0;
+    if (g < start + wn) {
+      uint64_t b, rs, re;
+      bool first, only;
+      if (kPlanned) {
+        b = a.pblk[g];
+        const uint64_t s0 = a.pstart[b], k = uint64_t(a.pstart[b + 1]) - s0, j = g - s0;
+        const uint64_t n = a.len[b];
+        re = n - (k - 1 - j) * a.piece_bytes;
+        rs = j ? n - (k - j) * a.piece_bytes : 0;
+        first = (j == 0);
+        only = (k == 1);
+      } else {
+        b = g;
+        rs = 0;
+        re = a.len[b];
+        first = true;
+        only = true;
+      }
+      const uintptr_t blk = reinterpret_cast<uintptr_t>(a.base) + a.off[b];
+      w_ps = blk + rs;
+      w_pe = blk + re;
+      w_b = uint32_t(b);
+      w_reg0 = first ? ~(a.init ? a.init[b] : 0u) : 0u;
+      w_only = only ? 1u : 0u;
+    }
   };
   struct Item {
     uint64_t g, b;
     uint32_t reg0;
     bool only;
   };
-  auto resolve = [&](Item& it, Staged<kG>& st) {  // descriptors -> byte range, then issue its loads
-    uint64_t b, rs, re;
-    bool first;
+  auto take = [&](uint64_t g, Item& it, Staged<kG>& st) {  // item g of the window -> stage its loads
+    const uint32_t i = uint32_t(g - w0);
+    // readlane returns int: go through uint32_t so nothing is sign-extended into the upper half
+    auto rl = [i](uint32_t v) -> uint32_t { return uint32_t(__builtin_amdgcn_readlane(int(v), int(i))); };
     it.g = g;
-    if (kPlanned) {
-      b = ldc(a.pblk, g);
-      const uint64_t s0 = ldc(a.pstart, b), k = uint64_t(ldc(a.pstart, b + 1)) - s0, j = g - s0;
-      const uint64_t n = ldc(a.len, b);
-      re = n - (k - 1 - j) * a.piece_bytes;
-      rs = j ? n - (k - j) * a.piece_bytes : 0;
-      first = (j == 0);
-      it.only = (k == 1);
-    } else {
-      b = g;
-      rs = 0;
-      re = ldc(a.len, b);
-      first = true;
-      it.only = true;
+    it.b = rl(w_b);
+    it.reg0 = rl(w_reg0);
+    it.only = rl(w_only) != 0;
+    const uintptr_t ps = (uintptr_t(rl(uint32_t(w_ps >> 32))) << 32) | uintptr_t(rl(uint32_t(w_ps)));
+    const uintptr_t pe = (uintptr_t(rl(uint32_t(w_pe >> 32))) << 32) | uintptr_t(rl(uint32_t(w_pe)));
+    stage<kG, kNT>(st, ps, pe, lane, reinterpret_cast<uintptr_t>(a.tabs));
+  };
+  auto emit = [&](const Item& it, uint32_t reg) {
+    if (lane == 0) {
+      if (it.only) emit_block(a, it.b, ~reg);
+      else a.partial[it.g] = reg;
     }
-    it.b = b;
-    it.reg0 = first ? ~(a.init ? ldc(a.init, b) : 0u) : 0u;
-    const uintptr_t blk = reinterpret_cast<uintptr_t>(a.base) + ldc(a.off, b);
-    stage<kG, kNT>(st, blk + rs, blk + re, lane, reinterpret_cast<uintptr_t>(a.tabs));
   };
 
   Item cur, nxt;
   Staged<kG> S, T;
-  bool have = next();
-  if (have) resolve(cur, S);
-  while (have) {
-    bool hn = false;
-    if (kAhead) {  // the next item's HBM loads overlap this item's compute
-      hn = next();
-      if (hn) resolve(nxt, T);
+  while (grab()) {
+    for (uint64_t ws = lo; ws < hi; ws += 64) {
+      fill(ws, hi);
+      take(w0, cur, S);
+      for (uint64_t g = w0; g < w0 + wn; ++g) {
+        const bool hn = g + 1 < w0 + wn;
+        if (kAhead && hn) take(g + 1, nxt, T);  // the next item's HBM loads overlap this item's compute
+        emit(cur, finish<kG, kNT, kAbl>(lds, S, cur.reg0, lane, lc0, lc1));
+        if (!kAhead && hn) take(g + 1, nxt, T);
+        cur = nxt;
+        S = T;
+      }
     }
-    const uint32_t reg = finish<kG, kNT, kAbl>(lds, S, cur.reg0, lane, lc0, lc1);
-    if (lane == 0) {
-      if (cur.only) emit_block(a, cur.b, ~reg);
-      else a.partial[cur.g] = reg;
-    }
-    if (!kAhead) {
-      hn = next();
-      if (hn) resolve(nxt, T);
-    }
-    cur = nxt;
-    S = T;
-    have = hn;
   }
 }
 
