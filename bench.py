@@ -65,8 +65,29 @@ def load_oracle():
     return _lo()
 
 
+class RefBatch:
+    """oracle/_ref/libref_crc32c.so: the reference's own util/crc32c.cc compiled -O3 (oracle/Makefile)
+    plus a threaded batch driver (oracle/ref_shim.cc).  Built in the dev container, shipped as a binary."""
+
+    PATH = os.path.join(ROOT, "oracle", "_ref", "libref_crc32c.so")
+
+    def __init__(self):
+        self.lib = ctypes.CDLL(self.PATH)
+        self.lib.ref_crc32c_batch.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_int]
+        self.lib.ref_crc32c_batch.restype = ctypes.c_int
+
+    def batch(self, buf, off, length, init=None, threads=1):
+        out = np.zeros(off.size, dtype=np.uint32)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint64)
+        assert self.lib.ref_crc32c_batch(buf.ctypes.data, off.ctypes.data, length.ctypes.data, None,
+                                         out.ctypes.data, off.size, threads) == 0
+        return out
+
+
 def cpu_baseline(oracle, data_dev, off, ln, sample_blocks, threads):
-    """Oracle (a restatement of util/crc32c.cc's portable path, compiled -O3) on host cores."""
+    """CPU CRC on host cores over a sample of the batch: the compiled reference (kind "reference")
+    when oracle/_ref was built, else the oracle restatement (kind "port")."""
     idx = np.linspace(0, off.size - 1, sample_blocks).astype(np.int64)
     lens = ln[idx]
     host = np.empty(int(lens.sum()), dtype=np.uint8)
@@ -78,15 +99,18 @@ def cpu_baseline(oracle, data_dev, off, ln, sample_blocks, threads):
         hoff[k] = pos
         pos += n
     out = {}
+    impl, kind = oracle, "port"
+    if os.path.exists(RefBatch.PATH):
+        impl, kind = RefBatch(), "reference"
     for t in sorted({1, threads}):
         sub = sample_blocks if t > 1 else max(1, sample_blocks // 4)
         sb = int(lens[:sub].sum())
-        oracle.batch(host, hoff[:min(sub, 8)], lens[:min(sub, 8)], threads=1)  # warm tables
+        impl.batch(host, hoff[:min(sub, 8)], lens[:min(sub, 8)], threads=1)  # warm tables
         t0 = time.perf_counter()
-        res = oracle.batch(host, hoff[:sub], lens[:sub], threads=t)
+        res = impl.batch(host, hoff[:sub], lens[:sub], threads=t)
         dt = time.perf_counter() - t0
         out[t] = (sb / GIB / dt, sb, dt)
-    return out, host, hoff, lens, idx
+    return out, host, hoff, lens, idx, kind
 
 
 def host_roundtrip(ctx, nbytes_target: int):
@@ -130,10 +154,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if os.environ.get("KVSEP_BENCH_SAME_DEVICE"):  # rehearsal: every rank on cuda:0, gloo for results
+            local = 0
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    coll_dev = dev if world == 1 or dist.get_backend() == "nccl" else torch.device("cpu")
 
     ctx = kvsep.Context(local)
     if args.piece_kib:
@@ -178,7 +207,7 @@ def main():
     elapsed = time.perf_counter() - t0
     ctx.set_timing(False)
     kern_ms, launches = ctx.get_timing()
-    elapsed = shard.max_over_ranks(elapsed, dist if world > 1 else None, dev)
+    elapsed = shard.max_over_ranks(elapsed, dist if world > 1 else None, coll_dev)
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * useful * args.steps / GIB / elapsed
     kern_avg_ms = kern_ms / max(1, launches)
@@ -187,7 +216,7 @@ def main():
     # ---- outside the timed region: result digest gather (RCCL), parity spot check, ceilings
     crcs = out.cpu().numpy().view(np.uint32)
     digest = shard.crc_of_crcs(crcs, kvsep.extend_host)
-    digests = shard.gather_digests(digest, dist if world > 1 else None, dev)
+    digests = shard.gather_digests(digest, dist if world > 1 else None, coll_dev)
 
     sink = torch.zeros(4, dtype=torch.int32, device=dev)
     ctx.stream_read(data.data_ptr(), span, sink, stream=stream)  # warm
@@ -207,15 +236,18 @@ def main():
         threads = min(args.cpu_threads, len(os.sched_getaffinity(0)))
         nsample = min(args.cpu_sample_blocks, count)
         if not args.no_cpu and world == 1:
-            res, host, hoff, lens, idx = cpu_baseline(oracle, data, off, ln, nsample, threads)
+            res, host, hoff, lens, idx, kind = cpu_baseline(oracle, data, off, ln, nsample, threads)
             exp = oracle.batch(host, hoff, lens, threads=threads)
             parity = bool(np.array_equal(exp, crcs[idx]))
             vt, sbt, dtt = res[threads]
             v1, sb1, dt1 = res[1]
-            cpu = {"value": round(vt, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            impl_desc = ("util/crc32c.cc of the reference (portable path, g++ -O3, oracle/_ref)"
+                         if kind == "reference" else
+                         "oracle/crc32c_oracle.c (restated util/crc32c.cc portable path, gcc -O3)")
+            cpu = {"value": round(vt, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
                    "sample": f"{nsample} blocks of the same batch ({sbt / GIB:.2f} GiB) copied to host memory, "
-                             f"oracle/crc32c_oracle.c (restated util/crc32c.cc portable path, gcc -O3), "
-                             f"{threads} threads split by bytes; 1 thread: {v1:.3f} GiB/s on {sb1 / GIB:.2f} GiB",
+                             f"{impl_desc}, {threads} threads split by bytes; 1 thread: {v1:.3f} GiB/s on "
+                             f"{sb1 / GIB:.2f} GiB",
                    "single_thread_GiBps": round(v1, 3)}
         else:
             idx = np.linspace(0, count - 1, 16).astype(np.int64)

@@ -15,3 +15,47 @@ uint32_t ref_crc32c_value(const char* data, size_t n) { return leveldb::crc32c::
 uint32_t ref_crc32c_mask(uint32_t c) { return leveldb::crc32c::Mask(c); }
 uint32_t ref_crc32c_unmask(uint32_t m) { return leveldb::crc32c::Unmask(m); }
 }
+
+// Batched driver over the reference Extend (same contract as oracle_crc32c_batch): blocks split over
+// `nthreads` host threads by contiguous byte-balanced ranges.  Used as bench.py's cpu_baseline
+// ("reference" kind) so the baseline is the reference's own code, compiled -O3.
+#include <pthread.h>
+
+namespace {
+struct RefJob {
+  const char* base; const uint64_t* off; const uint64_t* len; const uint32_t* init; uint32_t* out;
+  size_t lo, hi;
+};
+void* ref_worker(void* p) {
+  RefJob* j = static_cast<RefJob*>(p);
+  for (size_t i = j->lo; i < j->hi; ++i)
+    j->out[i] = leveldb::crc32c::Extend(j->init ? j->init[i] : 0u, j->base + j->off[i], j->len[i]);
+  return nullptr;
+}
+}  // namespace
+
+extern "C" int ref_crc32c_batch(const char* base, const uint64_t* off, const uint64_t* len, const uint32_t* init,
+                                uint32_t* out, size_t count, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  uint64_t total = 0;
+  for (size_t i = 0; i < count; ++i) total += len[i];
+  pthread_t th[256];
+  RefJob jobs[256];
+  size_t start = 0;
+  uint64_t acc = 0;
+  int launched = 0;
+  for (int t = 0; t < nthreads && start < count; ++t) {
+    const uint64_t target = (total / uint64_t(nthreads)) * uint64_t(t + 1);
+    size_t stop = start;
+    if (t == nthreads - 1) stop = count;
+    else
+      while (stop < count && acc < target) acc += len[stop++];
+    jobs[t] = RefJob{base, off, len, init, out, start, stop};
+    if (pthread_create(&th[t], nullptr, ref_worker, &jobs[t]) != 0) return -1;
+    ++launched;
+    start = stop;
+  }
+  for (int t = 0; t < launched; ++t) pthread_join(th[t], nullptr);
+  return 0;
+}
