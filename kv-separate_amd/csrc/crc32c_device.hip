@@ -283,9 +283,15 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
   const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerWg;
 
   uint64_t total = a.count;
+  bool planned = kPlanned;
   if (kPlanned) {
     total = ldc(a.pstart, a.count);
-    if (total > a.max_pieces) total = a.max_pieces;  // scratch overflow guard (caller bound violated)
+    // More pieces than scratch (the caller under-stated total_bytes): do not split at all -- one work
+    // item per block is slower for long blocks but exact; the combine kernel then skips every block.
+    if (total > a.max_pieces) {
+      planned = false;
+      total = a.count;
+    }
   }
 
   // Work distribution.  Static: wave w owns the run [w*per, (w+1)*per) (or round-robin single items).
@@ -332,7 +338,7 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
     if (g < start + wn) {
       uint64_t b, rs, re;
       bool first, only;
-      if (kPlanned) {
+      if (planned) {
         b = a.pblk[g];
         const uint64_t s0 = a.pstart[b], k = uint64_t(a.pstart[b + 1]) - s0, j = g - s0;
         const uint64_t n = a.len[b];
@@ -405,7 +411,7 @@ __global__ void __launch_bounds__(256) crc32c_combine_kernel(PiecesArgs a) {
   const uint64_t b = uint64_t(blockIdx.x) * 256 + threadIdx.x;
   if (b >= a.count) return;
   const uint32_t s = a.pstart[b], e = a.pstart[b + 1];
-  if (e - s <= 1 || e > a.max_pieces) return;
+  if (e - s <= 1 || a.pstart[a.count] > a.max_pieces) return;  // unsplit fallback: already emitted
   uint32_t acc = a.partial[s];
   for (uint32_t g = s + 1; g < e; ++g) {
     acc = zp[acc & 255u] ^ zp[256 + ((acc >> 8) & 255u)] ^ zp[512 + ((acc >> 16) & 255u)] ^ zp[768 + (acc >> 24)];

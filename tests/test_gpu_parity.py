@@ -259,3 +259,21 @@ def test_split_invariance_full_cfg3_scale(ctx):
     first = run(ctx, d, off, k)
     rest = run(ctx, d, off + k, ln - k, first)
     assert np.array_equal(whole, rest)
+
+
+def test_understated_total_bytes_still_exact(oracle):
+    """total_bytes only sizes scratch: if the caller under-states it, blocks are processed unsplit
+    (slower) but results stay exact."""
+    c = kvsep.Context(0)
+    try:
+        off, ln = W.cfg4_layout(600)
+        span = int(off[-1] + ln[-1])
+        d = torch.empty(span + 64, dtype=torch.uint8, device=DEV)
+        kvsep.fill_splitmix64(d.data_ptr(), span, 31, 0)
+        exp = oracle.batch(d[:span].cpu().numpy(), off, ln, threads=8)
+        out = torch.zeros(off.size, dtype=torch.int32, device=DEV)
+        c.batch_device(d.data_ptr(), dev_u64(off), dev_u64(ln), out, total_bytes=0, max_len=0)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), exp)
+    finally:
+        c.close()
