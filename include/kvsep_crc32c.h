@@ -127,6 +127,11 @@ int kvsep_sst_verify_device(kvsep_crc32c_ctx* ctx, void* stream, const void* fil
                             const uint64_t* len, uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count,
                             uint64_t total_bytes, uint64_t max_len);
 
+/* Pinned (page-locked) host memory for file images: read a vlog / SST file straight into it and the
+ * host-span entry points DMA from it directly, without the staging memcpy.  NULL on failure. */
+void* kvsep_host_alloc_pinned(uint64_t bytes);
+void kvsep_host_free_pinned(void* p);
+
 /* ---------------------------------------------------------------- support
  * Synthetic data: byte i of the stream is byte (i&7) of splitmix64 word (i>>3) of `seed`
  * (word j = mix(seed + (j+1)*0x9E3779B97F4A7C15)); writes bytes [stream_offset, +nbytes) to dst. */

@@ -402,6 +402,20 @@ int kvsep_crc32c_batch_host(kvsep_crc32c_ctx* c, const uint32_t* init, const cha
   return KVSEP_OK;
 }
 
+void* kvsep_host_alloc_pinned(uint64_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    set_last_error("hipHostMalloc failed");
+    return nullptr;
+  }
+  return p;
+}
+
+void kvsep_host_free_pinned(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
 const char* kvsep_build_info(void) {
   return "kvsep_crc32c: gfx950 HIP kernels (LDS-replicated Z_1024 stride chains, v_perm addressing), "
          "host SSE4.2 path, ABI 1";

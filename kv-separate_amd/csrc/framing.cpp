@@ -10,14 +10,11 @@
 //              block, then a 5-byte trailer [type u8][Mask(Extend(Value(block), &type, 1)) LE32].
 //
 // The serial parts (header walks) stay on the host; every checksum goes through one batched call.
-#include <hip/hip_runtime.h>
-
 #include <cstdint>
 #include <cstring>
 #include <vector>
 
 #include "../../include/kvsep_crc32c.h"
-#include "kvsep_internal.h"
 
 namespace {
 

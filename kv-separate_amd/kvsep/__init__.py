@@ -91,6 +91,8 @@ _SIGS = {
     "kvsep_sst_verify_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]),
+    "kvsep_host_alloc_pinned": (ctypes.c_void_p, [ctypes.c_uint64]),
+    "kvsep_host_free_pinned": (None, [ctypes.c_void_p]),
     "kvsep_last_error": (ctypes.c_char_p, []),
     "kvsep_build_info": (ctypes.c_char_p, []),
     "kvsep_device_count": (ctypes.c_int, []),
