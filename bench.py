@@ -121,7 +121,11 @@ def host_roundtrip(ctx, nbytes_target: int):
     dev = torch.empty(span, dtype=torch.uint8, device="cuda")
     kvsep.fill_splitmix64(dev.data_ptr(), span, 77, 0)
     buf.copy_(dev)
+    ref = torch.zeros(off.size, dtype=torch.int32, device="cuda")  # same records, device-resident path
+    ctx.batch_device(dev.data_ptr(), to_dev_u64(off, dev.device), to_dev_u64(ln, dev.device), ref,
+                     total_bytes=int(ln.sum()), max_len=int(ln.max()))
     torch.cuda.synchronize()
+    ref = ref.cpu().numpy().view(np.uint32)
     del dev
     arr = buf.numpy()
     ctx.batch_host_span(arr, off, ln)  # warm staging
@@ -130,7 +134,7 @@ def host_roundtrip(ctx, nbytes_target: int):
     for _ in range(reps):
         res = ctx.batch_host_span(arr, off, ln)
     dt = (time.perf_counter() - t0) / reps
-    return float(ln.sum()) / GIB / dt, int(ln.sum()), res
+    return float(ln.sum()) / GIB / dt, int(ln.sum()), bool(np.array_equal(res, ref))
 
 
 def main():
@@ -256,9 +260,10 @@ def main():
             parity = bool(list(crcs[idx]) == exp)
 
     rt = None
+    rt_ok = None
     if rank == 0 and world == 1 and args.roundtrip_gib > 0:
         try:
-            rt_gibps, rt_bytes, _ = host_roundtrip(ctx, int(args.roundtrip_gib * GIB))
+            rt_gibps, rt_bytes, rt_ok = host_roundtrip(ctx, int(args.roundtrip_gib * GIB))
             rt = round(rt_gibps, 3)
         except Exception as e:  # keep the headline line even if pinned allocation is refused
             log(f"host round trip failed: {e}")
@@ -297,6 +302,7 @@ def main():
             "read_ceiling_GBps": round(read_ceiling_gbps, 1),
             "frac_of_read_ceiling": round(achieved_gbps / read_ceiling_gbps, 4),
             "host_roundtrip_GiBps": rt,
+            "host_roundtrip_parity": rt_ok,
             "parity_spot_check": parity,
             "digests": [hex(d) for d in digests],
         }

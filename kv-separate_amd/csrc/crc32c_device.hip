@@ -521,19 +521,7 @@ struct kvsep_crc32c_ctx {
   int dynamic = -1;  // -1 auto, 0 static, 1 guided
   int variant = 1;   // rows per prefetch group / load policy, see launch_pieces
   uint32_t static_contig = 1;
-  // scratch
-  uint64_t cap_count = 0, cap_pieces = 0;
-  uint32_t* d_counts = nullptr;
-  uint32_t* d_pstart = nullptr;
-  uint32_t* d_pblk = nullptr;
-  uint32_t* d_partial = nullptr;
-  uint32_t* d_counter = nullptr;
-  unsigned long long* d_verify_scratch = nullptr;  // [first_bad, nbad] when the caller passes none
-  uint64_t* d_sst_len1 = nullptr;   // SST verify scratch: len + 1 ...
-  uint32_t* d_sst_stored = nullptr; // ... and the stored trailer words
-  uint64_t cap_sst = 0;
-  void* d_scan_tmp = nullptr;
-  size_t scan_tmp_bytes = 0;
+  Scratch sc;  // scratch of the calls made directly on this context (any stream, event-ordered)
   // timing
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
@@ -574,32 +562,53 @@ int upload_tables(kvsep_crc32c_ctx* c) {
   return KVSEP_OK;
 }
 
-void free_scratch(kvsep_crc32c_ctx* c) {
-  hipFree(c->d_counts); hipFree(c->d_pstart); hipFree(c->d_pblk); hipFree(c->d_partial);
-  hipFree(c->d_scan_tmp);
-  c->d_counts = c->d_pstart = c->d_pblk = c->d_partial = nullptr;
-  c->d_scan_tmp = nullptr;
-  c->cap_count = c->cap_pieces = 0;
-  c->scan_tmp_bytes = 0;
+void free_plan(Scratch& sc) {
+  hipFree(sc.d_counts); hipFree(sc.d_pstart); hipFree(sc.d_pblk); hipFree(sc.d_partial);
+  hipFree(sc.d_scan_tmp);
+  sc.d_counts = sc.d_pstart = sc.d_pblk = sc.d_partial = nullptr;
+  sc.d_scan_tmp = nullptr;
+  sc.cap_count = sc.cap_pieces = 0;
+  sc.scan_tmp_bytes = 0;
 }
 
-int ensure_scratch(kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes) {
-  const uint64_t pieces = count + total_bytes / c->piece_bytes + 1;
+// Wait until the scratch's previous user (on whatever stream) is done with it -- before a realloc.
+int quiesce(Scratch& sc) {
+  if (sc.used && sc.last_use) KVSEP_HIP(hipEventSynchronize(sc.last_use));
+  return KVSEP_OK;
+}
+
+// Order this call behind the scratch's previous user when it ran on another stream.
+int acquire(Scratch& sc, hipStream_t s) {
+  if (!sc.last_use) KVSEP_HIP(hipEventCreateWithFlags(&sc.last_use, hipEventDisableTiming));
+  if (sc.used && sc.last_stream != s) KVSEP_HIP(hipStreamWaitEvent(s, sc.last_use, 0));
+  return KVSEP_OK;
+}
+
+int release(Scratch& sc, hipStream_t s) {
+  KVSEP_HIP(hipEventRecord(sc.last_use, s));
+  sc.last_stream = s;
+  sc.used = true;
+  return KVSEP_OK;
+}
+
+int ensure_plan(Scratch& sc, uint64_t piece_bytes, uint64_t count, uint64_t total_bytes) {
+  const uint64_t pieces = count + total_bytes / piece_bytes + 1;
   if (count > 0xffffffffull || pieces > 0xffffffffull) return set_err(KVSEP_EINVAL, "batch too large for u32 piece indices");
-  if (count <= c->cap_count && pieces <= c->cap_pieces) return KVSEP_OK;
-  const uint64_t nc = std::max<uint64_t>(count, c->cap_count), np = std::max<uint64_t>(pieces, c->cap_pieces);
-  KVSEP_HIP(hipDeviceSynchronize());
-  free_scratch(c);
-  KVSEP_HIP(hipMalloc(&c->d_counts, nc * 4));
-  KVSEP_HIP(hipMalloc(&c->d_pstart, (nc + 1) * 4));
-  KVSEP_HIP(hipMalloc(&c->d_pblk, np * 4));
-  KVSEP_HIP(hipMalloc(&c->d_partial, np * 4));
+  if (count <= sc.cap_count && pieces <= sc.cap_pieces) return KVSEP_OK;
+  const uint64_t nc = std::max<uint64_t>(count, sc.cap_count), np = std::max<uint64_t>(pieces, sc.cap_pieces);
+  int rc = quiesce(sc);
+  if (rc) return rc;
+  free_plan(sc);
+  KVSEP_HIP(hipMalloc(&sc.d_counts, nc * 4));
+  KVSEP_HIP(hipMalloc(&sc.d_pstart, (nc + 1) * 4));
+  KVSEP_HIP(hipMalloc(&sc.d_pblk, np * 4));
+  KVSEP_HIP(hipMalloc(&sc.d_partial, np * 4));
   size_t tb = 0;
-  KVSEP_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, c->d_counts, c->d_pstart + 1, int(nc), hipStream_t(0)));
-  KVSEP_HIP(hipMalloc(&c->d_scan_tmp, tb));
-  c->scan_tmp_bytes = tb;
-  c->cap_count = nc;
-  c->cap_pieces = np;
+  KVSEP_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, sc.d_counts, sc.d_pstart + 1, int(nc), hipStream_t(0)));
+  KVSEP_HIP(hipMalloc(&sc.d_scan_tmp, tb));
+  sc.scan_tmp_bytes = tb;
+  sc.cap_count = nc;
+  sc.cap_pieces = np;
   return KVSEP_OK;
 }
 
@@ -638,11 +647,26 @@ void launch_pieces(bool planned, bool dyn, int variant, unsigned grid, hipStream
   }
 }
 
-int launch_batch(kvsep_crc32c_ctx* c, hipStream_t s, const void* base, const uint64_t* off, const uint64_t* len,
-                 const uint32_t* init, const uint32_t* expect, uint32_t* out, uint64_t* first_bad, uint64_t* nbad,
-                 uint64_t count, uint64_t total_bytes, uint64_t max_len) {
+int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* base, const uint64_t* off,
+                    const uint64_t* len, const uint32_t* init, const uint32_t* expect, uint32_t* out,
+                    uint64_t* first_bad, uint64_t* nbad, uint64_t count, uint64_t total_bytes, uint64_t max_len);
+
+// Every use of a Scratch is bracketed by acquire/release (event ordering across streams).
+int launch_batch(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* base, const uint64_t* off,
+                 const uint64_t* len, const uint32_t* init, const uint32_t* expect, uint32_t* out, uint64_t* first_bad,
+                 uint64_t* nbad, uint64_t count, uint64_t total_bytes, uint64_t max_len) {
   if (!base || !off || !len || !out) return set_err(KVSEP_EINVAL, "null pointer argument");
   KVSEP_HIP(hipSetDevice(c->device));
+  int rc = acquire(sc, s);
+  if (rc) return rc;
+  rc = launch_batch_in(c, sc, s, base, off, len, init, expect, out, first_bad, nbad, count, total_bytes, max_len);
+  if (rc) return rc;
+  return release(sc, s);
+}
+
+int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* base, const uint64_t* off,
+                    const uint64_t* len, const uint32_t* init, const uint32_t* expect, uint32_t* out,
+                    uint64_t* first_bad, uint64_t* nbad, uint64_t count, uint64_t total_bytes, uint64_t max_len) {
   const bool planned = !(max_len != 0 && max_len <= c->piece_bytes);
   PiecesArgs a{};
   a.base = static_cast<const uint8_t*>(base);
@@ -656,9 +680,9 @@ int launch_batch(kvsep_crc32c_ctx* c, hipStream_t s, const void* base, const uin
   a.tabs = c->d_tabs;
   if (expect) {
     if (!first_bad || !nbad) {
-      if (!c->d_verify_scratch) KVSEP_HIP(hipMalloc(&c->d_verify_scratch, 16));
-      first_bad = reinterpret_cast<uint64_t*>(c->d_verify_scratch);
-      nbad = reinterpret_cast<uint64_t*>(c->d_verify_scratch + 1);
+      if (!sc.d_verify) KVSEP_HIP(hipMalloc(&sc.d_verify, 16));
+      first_bad = reinterpret_cast<uint64_t*>(sc.d_verify);
+      nbad = reinterpret_cast<uint64_t*>(sc.d_verify + 1);
     }
     a.first_bad = reinterpret_cast<unsigned long long*>(first_bad);
     a.nbad = reinterpret_cast<unsigned long long*>(nbad);
@@ -667,19 +691,19 @@ int launch_batch(kvsep_crc32c_ctx* c, hipStream_t s, const void* base, const uin
   }
   if (count == 0) return KVSEP_OK;
   if (planned) {
-    int rc = ensure_scratch(c, count, total_bytes);
+    int rc = ensure_plan(sc, c->piece_bytes, count, total_bytes);
     if (rc) return rc;
-    a.pstart = c->d_pstart;
-    a.pblk = c->d_pblk;
-    a.partial = c->d_partial;
-    a.max_pieces = c->cap_pieces;
+    a.pstart = sc.d_pstart;
+    a.pblk = sc.d_pblk;
+    a.partial = sc.d_partial;
+    a.max_pieces = sc.cap_pieces;
     const unsigned nb = unsigned((count + 255) / 256);
-    crc32c_plan_count_kernel<<<nb, 256, 0, s>>>(len, count, c->piece_bytes, c->d_counts);
+    crc32c_plan_count_kernel<<<nb, 256, 0, s>>>(len, count, c->piece_bytes, sc.d_counts);
     KVSEP_HIP(hipGetLastError());
-    KVSEP_HIP(hipMemsetAsync(c->d_pstart, 0, 4, s));
-    size_t tb = c->scan_tmp_bytes;
-    KVSEP_HIP(hipcub::DeviceScan::InclusiveSum(c->d_scan_tmp, tb, c->d_counts, c->d_pstart + 1, int(count), s));
-    crc32c_plan_expand_kernel<<<nb, 256, 0, s>>>(c->d_pstart, count, c->cap_pieces, c->d_pblk);
+    KVSEP_HIP(hipMemsetAsync(sc.d_pstart, 0, 4, s));
+    size_t tb = sc.scan_tmp_bytes;
+    KVSEP_HIP(hipcub::DeviceScan::InclusiveSum(sc.d_scan_tmp, tb, sc.d_counts, sc.d_pstart + 1, int(count), s));
+    crc32c_plan_expand_kernel<<<nb, 256, 0, s>>>(sc.d_pstart, count, sc.cap_pieces, sc.d_pblk);
     KVSEP_HIP(hipGetLastError());
   } else {
     a.max_pieces = count;
@@ -687,9 +711,9 @@ int launch_batch(kvsep_crc32c_ctx* c, hipStream_t s, const void* base, const uin
   const bool dyn = c->dynamic < 0 ? planned : c->dynamic == 1;  // auto: guided when planned, else static
   a.static_contig = c->static_contig;
   if (dyn) {
-    if (!c->d_counter) KVSEP_HIP(hipMalloc(&c->d_counter, 16));
-    a.work_counter = c->d_counter;
-    KVSEP_HIP(hipMemsetAsync(c->d_counter, 0, 4, s));
+    if (!sc.d_counter) KVSEP_HIP(hipMalloc(&sc.d_counter, 16));
+    a.work_counter = sc.d_counter;
+    KVSEP_HIP(hipMemsetAsync(sc.d_counter, 0, 4, s));
   }
   const unsigned grid = unsigned(c->num_cus);  // one 16-wave workgroup per CU, persistent
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -713,10 +737,21 @@ int launch_batch(kvsep_crc32c_ctx* c, hipStream_t s, const void* base, const uin
 }  // namespace
 
 namespace kvsep {
-int device_batch_locked(kvsep_crc32c_ctx* c, hipStream_t s, const void* base, const uint64_t* off,
+int device_batch_locked(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* base, const uint64_t* off,
                         const uint64_t* len, const uint32_t* init, uint32_t* out, uint64_t count,
                         uint64_t total_bytes, uint64_t max_len) {
-  return launch_batch(c, s, base, off, len, init, nullptr, out, nullptr, nullptr, count, total_bytes, max_len);
+  return launch_batch(c, sc, s, base, off, len, init, nullptr, out, nullptr, nullptr, count, total_bytes, max_len);
+}
+
+void free_scratch(Scratch& sc) {
+  if (sc.used && sc.last_use) (void)hipEventSynchronize(sc.last_use);
+  free_plan(sc);
+  hipFree(sc.d_counter);
+  hipFree(sc.d_verify);
+  hipFree(sc.d_sst_len1);
+  hipFree(sc.d_sst_stored);
+  if (sc.last_use) (void)hipEventDestroy(sc.last_use);
+  sc = Scratch();
 }
 HostStaging& ctx_staging(kvsep_crc32c_ctx* c) { return c->staging; }
 std::mutex& ctx_mutex(kvsep_crc32c_ctx* c) { return c->mu; }
@@ -764,12 +799,8 @@ void kvsep_crc32c_ctx_destroy(kvsep_crc32c_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);
   hipDeviceSynchronize();
-  free_scratch(c);
+  free_scratch(c->sc);
   hipFree(c->d_tabs);
-  hipFree(c->d_counter);
-  hipFree(c->d_verify_scratch);
-  hipFree(c->d_sst_len1);
-  hipFree(c->d_sst_stored);
   for (auto& p : c->ev_pending) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
   for (auto e : c->ev_pool) hipEventDestroy(e);
   release_staging(c->staging);
@@ -782,7 +813,8 @@ int kvsep_crc32c_ctx_set_piece_bytes(kvsep_crc32c_ctx* c, uint64_t piece_bytes) 
   KVSEP_HIP(hipSetDevice(c->device));
   KVSEP_HIP(hipDeviceSynchronize());
   c->piece_bytes = piece_bytes;
-  free_scratch(c);
+  free_plan(c->sc);  // piece tables depend on piece_bytes (device already idle)
+  for (auto& sc : c->staging.scratch) free_plan(sc);
   return upload_tables(c);
 }
 
@@ -796,7 +828,7 @@ int kvsep_crc32c_reserve(kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_byt
   if (!c) return set_err(KVSEP_EINVAL, "null ctx");
   std::lock_guard<std::mutex> g(c->mu);
   KVSEP_HIP(hipSetDevice(c->device));
-  return ensure_scratch(c, count, total_bytes);
+  return ensure_plan(c->sc, c->piece_bytes, count, total_bytes);
 }
 
 int kvsep_crc32c_ctx_set_timing(kvsep_crc32c_ctx* c, int enable) {
@@ -830,8 +862,8 @@ int kvsep_crc32c_batch_device(kvsep_crc32c_ctx* c, void* stream, const void* bas
                               uint64_t total_bytes, uint64_t max_len) {
   if (!c) return set_err(KVSEP_EINVAL, "null ctx");
   std::lock_guard<std::mutex> g(c->mu);
-  return launch_batch(c, static_cast<hipStream_t>(stream), base, off, len, init, nullptr, out, nullptr, nullptr,
-                      count, total_bytes, max_len);
+  return launch_batch(c, c->sc, static_cast<hipStream_t>(stream), base, off, len, init, nullptr, out, nullptr,
+                      nullptr, count, total_bytes, max_len);
 }
 
 int kvsep_crc32c_verify_device(kvsep_crc32c_ctx* c, void* stream, const void* base, const uint64_t* off,
@@ -840,8 +872,8 @@ int kvsep_crc32c_verify_device(kvsep_crc32c_ctx* c, void* stream, const void* ba
                                uint64_t total_bytes, uint64_t max_len) {
   if (!c || !expected_masked) return set_err(KVSEP_EINVAL, "null ctx or expected_masked");
   std::lock_guard<std::mutex> g(c->mu);
-  return launch_batch(c, static_cast<hipStream_t>(stream), base, off, len, init, expected_masked, out, first_bad,
-                      nbad, count, total_bytes, max_len);
+  return launch_batch(c, c->sc, static_cast<hipStream_t>(stream), base, off, len, init, expected_masked, out,
+                      first_bad, nbad, count, total_bytes, max_len);
 }
 
 int kvsep_fill_splitmix64_device(void* stream, void* dst, uint64_t nbytes, uint64_t seed, uint64_t stream_offset) {
@@ -869,8 +901,8 @@ int kvsep_sst_trailers_device(kvsep_crc32c_ctx* c, void* stream, const void* bas
   if (!c || !types || !masked_out) return set_err(KVSEP_EINVAL, "null argument");
   std::lock_guard<std::mutex> g(c->mu);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  int rc = launch_batch(c, s, base, off, len, nullptr, nullptr, masked_out, nullptr, nullptr, count, total_bytes,
-                        max_len);
+  int rc = launch_batch(c, c->sc, s, base, off, len, nullptr, nullptr, masked_out, nullptr, nullptr, count,
+                        total_bytes, max_len);
   if (rc || !count) return rc;
   sst_trailer_finish_kernel<<<unsigned((count + 255) / 256), 256, 0, s>>>(masked_out, types, masked_out, count,
                                                                           c->d_tabs);
@@ -885,24 +917,30 @@ int kvsep_sst_verify_device(kvsep_crc32c_ctx* c, void* stream, const void* file_
   std::lock_guard<std::mutex> g(c->mu);
   hipStream_t s = static_cast<hipStream_t>(stream);
   KVSEP_HIP(hipSetDevice(c->device));
-  if (count > c->cap_sst) {
-    KVSEP_HIP(hipStreamSynchronize(s));
-    hipFree(c->d_sst_len1);
-    hipFree(c->d_sst_stored);
-    c->d_sst_len1 = nullptr;
-    c->d_sst_stored = nullptr;
-    c->cap_sst = 0;
-    KVSEP_HIP(hipMalloc(&c->d_sst_len1, count * 8));
-    KVSEP_HIP(hipMalloc(&c->d_sst_stored, count * 4));
-    c->cap_sst = count;
+  Scratch& sc = c->sc;
+  int rc = acquire(sc, s);
+  if (rc) return rc;
+  if (count > sc.cap_sst) {
+    rc = quiesce(sc);
+    if (rc) return rc;
+    hipFree(sc.d_sst_len1);
+    hipFree(sc.d_sst_stored);
+    sc.d_sst_len1 = nullptr;
+    sc.d_sst_stored = nullptr;
+    sc.cap_sst = 0;
+    KVSEP_HIP(hipMalloc(&sc.d_sst_len1, count * 8));
+    KVSEP_HIP(hipMalloc(&sc.d_sst_stored, count * 4));
+    sc.cap_sst = count;
   }
   if (count) {
     sst_verify_prep_kernel<<<unsigned((count + 255) / 256), 256, 0, s>>>(static_cast<const uint8_t*>(file_base), off,
-                                                                        len, c->d_sst_len1, c->d_sst_stored, count);
+                                                                        len, sc.d_sst_len1, sc.d_sst_stored, count);
     KVSEP_HIP(hipGetLastError());
   }
-  return launch_batch(c, s, file_base, off, c->d_sst_len1, nullptr, c->d_sst_stored, out, first_bad, nbad, count,
-                      total_bytes + count, max_len ? max_len + 1 : 0);
+  rc = launch_batch_in(c, sc, s, file_base, off, sc.d_sst_len1, nullptr, sc.d_sst_stored, out, first_bad, nbad, count,
+                       total_bytes + count, max_len ? max_len + 1 : 0);
+  if (rc) return rc;
+  return release(sc, s);
 }
 
 int kvsep_stream_read_device(kvsep_crc32c_ctx* c, void* stream, const void* src, uint64_t nbytes, uint32_t* sink) {

@@ -28,6 +28,7 @@ void release_staging(HostStaging& s) {
     hipHostFree(s.h_data[i]); hipHostFree(s.h_desc[i]); hipHostFree(s.h_init[i]); hipHostFree(s.h_out[i]);
     hipFree(s.d_data[i]); hipFree(s.d_desc[i]); hipFree(s.d_init[i]); hipFree(s.d_out[i]);
     if (s.done[i]) hipEventDestroy(s.done[i]);
+    free_scratch(s.scratch[i]);
     if (s.stream[i]) hipStreamDestroy(s.stream[i]);
   }
   s = HostStaging();
@@ -188,8 +189,9 @@ int submit(kvsep_crc32c_ctx* c, HostStaging& s, int slot, uint64_t nblk, uint64_
   KVSEP_HIPH(hipMemcpyAsync(s.d_desc[slot] + s.max_blocks, s.h_desc[slot] + s.max_blocks, nblk * 8,
                             hipMemcpyHostToDevice, st));
   if (have_init) KVSEP_HIPH(hipMemcpyAsync(s.d_init[slot], s.h_init[slot], nblk * 4, hipMemcpyHostToDevice, st));
-  int rc = device_batch_locked(c, st, s.d_data[slot], s.d_desc[slot], s.d_desc[slot] + s.max_blocks,
-                               have_init ? s.d_init[slot] : nullptr, s.d_out[slot], nblk, payload, max_len);
+  int rc = device_batch_locked(c, s.scratch[slot], st, s.d_data[slot], s.d_desc[slot],
+                               s.d_desc[slot] + s.max_blocks, have_init ? s.d_init[slot] : nullptr, s.d_out[slot],
+                               nblk, payload, max_len);
   if (rc) return rc;
   KVSEP_HIPH(hipMemcpyAsync(s.h_out[slot], s.d_out[slot], nblk * 4, hipMemcpyDeviceToHost, st));
   KVSEP_HIPH(hipEventRecord(s.done[slot], st));
@@ -222,8 +224,8 @@ int big_block(kvsep_crc32c_ctx* c, HostStaging& s, SlotJob* jobs, uint32_t* out,
     } else {  // seed with the previous segment's CRC, straight from device memory
       KVSEP_HIPH(hipMemcpyAsync(s.d_init[slot], s.d_out[slot ^ 1], 4, hipMemcpyDeviceToDevice, st));
     }
-    int rc = device_batch_locked(c, st, s.d_data[slot], s.d_desc[slot], s.d_desc[slot] + s.max_blocks,
-                                 s.d_init[slot], s.d_out[slot], 1, seg, seg);
+    int rc = device_batch_locked(c, s.scratch[0], st, s.d_data[slot], s.d_desc[slot],
+                                 s.d_desc[slot] + s.max_blocks, s.d_init[slot], s.d_out[slot], 1, seg, seg);
     if (rc) return rc;
     KVSEP_HIPH(hipEventRecord(s.done[slot], st));
   }

@@ -10,6 +10,29 @@ struct kvsep_crc32c_ctx;
 
 namespace kvsep {
 
+// Device scratch of one in-flight batch: the piece plan (planned mode), the work counter, the verify
+// defaults and the SST-verify arrays.  A scratch object is reused call after call; `last_use` orders a
+// call on a different stream behind the previous user, so reuse across streams is race-free.  The host
+// pipeline gives each staging slot its own Scratch so the two slots' batches overlap.
+struct Scratch {
+  uint64_t cap_count = 0, cap_pieces = 0;
+  uint32_t* d_counts = nullptr;
+  uint32_t* d_pstart = nullptr;
+  uint32_t* d_pblk = nullptr;
+  uint32_t* d_partial = nullptr;
+  void* d_scan_tmp = nullptr;
+  size_t scan_tmp_bytes = 0;
+  uint32_t* d_counter = nullptr;
+  unsigned long long* d_verify = nullptr;  // [first_bad, nbad] when the caller passes none
+  uint64_t* d_sst_len1 = nullptr;           // SST verify: len + 1 ...
+  uint32_t* d_sst_stored = nullptr;         // ... and the stored trailer words
+  uint64_t cap_sst = 0;
+  hipEvent_t last_use = nullptr;
+  hipStream_t last_stream = nullptr;
+  bool used = false;
+};
+void free_scratch(Scratch& sc);
+
 // Double-buffered host<->device staging for the host-memory entry points.
 struct HostStaging {
   static constexpr int kSlots = 2;
@@ -25,13 +48,14 @@ struct HostStaging {
   uint32_t* d_out[kSlots] = {nullptr, nullptr};
   hipStream_t stream[kSlots] = {nullptr, nullptr};
   hipEvent_t done[kSlots] = {nullptr, nullptr};
+  Scratch scratch[kSlots];
   bool ready = false;
 };
 
 void release_staging(HostStaging& s);
 
 // Implemented in crc32c_device.hip; callers hold ctx_mutex.
-int device_batch_locked(kvsep_crc32c_ctx* c, hipStream_t s, const void* base, const uint64_t* off,
+int device_batch_locked(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* base, const uint64_t* off,
                         const uint64_t* len, const uint32_t* init, uint32_t* out, uint64_t count,
                         uint64_t total_bytes, uint64_t max_len);
 HostStaging& ctx_staging(kvsep_crc32c_ctx* c);

@@ -277,3 +277,37 @@ def test_understated_total_bytes_still_exact(oracle):
         assert np.array_equal(out.cpu().numpy().view(np.uint32), exp)
     finally:
         c.close()
+
+
+def test_host_span_long_blocks_pinned_and_pageable(ctx, oracle):
+    """Both staging slots run planned (split) batches concurrently: each slot owns its scratch."""
+    off, ln = W.cfg3_layout(vlog=True, count=200)
+    span = int(off[-1] + ln[-1])
+    d = torch.empty(span, dtype=torch.uint8, device=DEV)
+    kvsep.fill_splitmix64(d.data_ptr(), span, 41, 0)
+    pinned = torch.empty(span, dtype=torch.uint8, pin_memory=True)
+    pinned.copy_(d)
+    torch.cuda.synchronize()
+    host = pinned.numpy()
+    exp = oracle.batch(host, off, ln, threads=16)
+    for _ in range(3):
+        assert np.array_equal(ctx.batch_host_span(host, off, ln), exp)
+    assert np.array_equal(ctx.batch_host_span(host.copy(), off, ln), exp)  # pageable
+
+
+def test_one_context_two_streams(ctx, oracle):
+    """Back-to-back planned batches on two streams share the context scratch: event-ordered, exact."""
+    off, ln = W.cfg4_layout(3000)
+    span = int(off[-1] + ln[-1])
+    d = torch.empty(span + 64, dtype=torch.uint8, device=DEV)
+    kvsep.fill_splitmix64(d.data_ptr(), span, 43, 0)
+    exp = oracle.batch(d[:span].cpu().numpy(), off, ln, threads=16)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    d_off, d_len = dev_u64(off), dev_u64(ln)
+    outs = [torch.zeros(off.size, dtype=torch.int32, device=DEV) for _ in range(6)]
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        ctx.batch_device(d.data_ptr(), d_off, d_len, o, total_bytes=int(ln.sum()), stream=s1 if i % 2 else s2)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), exp)
