@@ -79,6 +79,16 @@ struct PiecesArgs {
   const DevTables* tabs;
 };
 
+#ifdef KVSEP_STAMPS  // diagnostic build: per-wave cycle sums of the work-loop segments
+__device__ unsigned long long g_kvsep_stamps[8192 * 4];
+#define KVSEP_STAMP(v)                                                                     \
+  do {                                                                                     \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");             \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+  } while (0)
+#endif
+
 // Descriptor reads through the constant address space: wave-uniform indices then lower to scalar
 // s_load (lgkmcnt), so fetching the next item's descriptors never drains the vmcnt of in-flight
 // payload loads.  Descriptors are read-only for the whole launch.
@@ -107,6 +117,12 @@ __device__ __forceinline__ uint32_t fold1024(const uint8_t* lds, uint32_t c, uin
   const uint32_t a2 = __builtin_amdgcn_perm(c, lc1, 0x0C020600u);
   const uint32_t a3 = __builtin_amdgcn_perm(c, lc1, 0x0C020700u);
   return lds_u32(lds, a0) ^ lds_u32(lds, a1 + 128u) ^ lds_u32(lds, a2) ^ lds_u32(lds, a3 + 128u);
+}
+
+// DPP row_shr:N -- lane l receives lane l - N of its 16-lane row (a VALU op, no LDS round trip).
+template <int N>
+__device__ __forceinline__ uint32_t row_shr(uint32_t v) {
+  return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x110 + N, 0xF, 0xF, false));
 }
 
 // Serial steps over bytes [q0, q1) of a 16-B aligned chunk (0 <= q0 <= q1 <= 16), wave-uniform.
@@ -230,14 +246,31 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     // pull the pending word of the segment 16*2^j bytes before theirs and carry it forward by 16*2^j.
     // Only those lanes touch LDS (exec-masked), which keeps the non-replicated tree tables' bank
     // conflicts small -- the tree is the LDS hot spot for short blocks.
+    // The partner of an active lane l is l - 2^j: DPP row_shr for j < 4 (within a 16-lane row), lane
+    // reads for j = 4, 5 -- no ds_bpermute round trips on this latency-bound chain.
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
-      const uint32_t o = __shfl_xor(p, 1 << j);
+      uint32_t o;
+      if (j == 0) {
+        o = row_shr<1>(p);
+      } else if (j == 1) {
+        o = row_shr<2>(p);
+      } else if (j == 2) {
+        o = row_shr<4>(p);
+      } else if (j == 3) {
+        o = row_shr<8>(p);
+      } else if (j == 4) {  // active lanes 31 and 63 need lanes 15 and 47
+        const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(p), 15));
+        const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(p), 47));
+        o = lane < 32 ? lo : hi;
+      } else {  // active lane 63 needs lane 31
+        o = uint32_t(__builtin_amdgcn_readlane(int(p), 31));
+      }
       const uint32_t m = (2u << j) - 1u;
       if ((lane & m) == m) p = zmap(lds, kTreeOff + 4096u * j, o) ^ p;
     }
-    p = __shfl(p, 63);               // pending word at a1 - 4
-    reg = zmap(lds, kZ4Off, p);      // register at a1
+    p = uint32_t(__builtin_amdgcn_readlane(int(p), 63));  // pending word at a1 - 4 (wave-uniform)
+    reg = zmap(lds, kZ4Off, p);                              // register at a1
   } else if (s.ps < s.h0) {
     reg = serial16(lds, reg, s.hc, int(s.ps - s.hbase), int(s.h0 - s.hbase));
   }
@@ -393,8 +426,28 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
       take(w0, cur, S);
       for (uint64_t g = w0; g < w0 + wn; ++g) {
         const bool hn = g + 1 < w0 + wn;
+#ifdef KVSEP_STAMPS  // diagnostic build only (kv-separate_amd/tools/stamp_probe.hip)
+        unsigned long long t0, t1, t2, t3;
+        KVSEP_STAMP(t0);
+#endif
         if (kAhead && hn) take(g + 1, nxt, T);  // the next item's HBM loads overlap this item's compute
+#ifdef KVSEP_STAMPS
+        KVSEP_STAMP(t1);
+        if (hn) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // this item's 7 loads, not the next's
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        KVSEP_STAMP(t2);
+#endif
         emit(cur, finish<kG, kNT, kAbl>(lds, S, cur.reg0, lane, lc0, lc1));
+#ifdef KVSEP_STAMPS
+        KVSEP_STAMP(t3);
+        if (lane == 0) {
+          unsigned long long* st = &g_kvsep_stamps[(uint64_t(blockIdx.x) * kWavesPerWg + wave) * 4];
+          st[0] += t1 - t0;
+          st[1] += t2 - t1;
+          st[2] += t3 - t2;
+          st[3] += 1;
+        }
+#endif
         if (!kAhead && hn) take(g + 1, nxt, T);
         cur = nxt;
         S = T;
