@@ -80,7 +80,8 @@ struct PiecesArgs {
 };
 
 #ifdef KVSEP_STAMPS  // diagnostic build: per-wave cycle sums of the work-loop segments
-__device__ unsigned long long g_kvsep_stamps[8192 * 4];
+__device__ unsigned long long g_kvsep_stamps[8192 * 8];
+#define KVSEP_RSTAMP(v) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory")
 #define KVSEP_STAMP(v)                                                                     \
   do {                                                                                     \
     __builtin_amdgcn_sched_barrier(0);                                                     \
@@ -123,6 +124,11 @@ __device__ __forceinline__ uint32_t fold1024(const uint8_t* lds, uint32_t c, uin
 template <int N>
 __device__ __forceinline__ uint32_t row_shr(uint32_t v) {
   return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x110 + N, 0xF, 0xF, false));
+}
+
+__device__ __forceinline__ uint4 uniform4(uint4 v) {
+  return make_uint4(uint32_t(__builtin_amdgcn_readfirstlane(int(v.x))), uint32_t(__builtin_amdgcn_readfirstlane(int(v.y))),
+                    uint32_t(__builtin_amdgcn_readfirstlane(int(v.z))), uint32_t(__builtin_amdgcn_readfirstlane(int(v.w))));
 }
 
 // Serial steps over bytes [q0, q1) of a 16-B aligned chunk (0 <= q0 <= q1 <= 16), wave-uniform.
@@ -178,7 +184,8 @@ struct Staged {
 // device address), so the compiler can wait for exactly this item's loads with a counted vmcnt
 // while the next item's loads stay in flight; masking is deferred to finish().
 template <int kG, bool kNT>
-__device__ __forceinline__ void stage(Staged<kG>& s, uintptr_t ps, uintptr_t pe, uint32_t lane, uintptr_t dummy) {
+__device__ __forceinline__ void stage(Staged<kG>& s, uintptr_t ps, uintptr_t pe, uint32_t lane, uintptr_t dummy,
+                                      uint32_t vz) {
   s.ps = ps;
   s.pe = pe;
   s.hbase = ps & ~uintptr_t(15);
@@ -189,8 +196,12 @@ __device__ __forceinline__ void stage(Staged<kG>& s, uintptr_t ps, uintptr_t pe,
   s.K = s.a1 > s.h0 ? (uint64_t(s.a1 - s.h0) + kRowBytes - 1) / kRowBytes : 0;
   s.seg = s.a1 - s.K * kRowBytes + uintptr_t(lane) * 16u;
   s.v_ok = s.K && s.seg >= s.h0;  // row 0 is front-masked: lanes before h0 hold zeros
-  s.hc = ld16(ps < s.h0 ? s.hbase : dummy);   // aligned 16 B holding the head (never crosses a page)
-  s.tc = ld16(s.a1 < pe ? s.a1 : dummy);      // aligned 16 B holding the tail
+  // Head and tail chunks are wave-uniform, but their addresses are offset by the opaque zero `vz` so the
+  // compiler keeps them in VGPRs: a provably uniform load result is moved to SGPRs with readfirstlane
+  // right here, which waits (vmcnt) for the NEXT item's first load inside the current item -- a full HBM
+  // latency per item.  finish() reads them out after this item's own wait instead.
+  s.hc = ld16((ps < s.h0 ? s.hbase : dummy) + vz);  // aligned 16 B holding the head (never crosses a page)
+  s.tc = ld16((s.a1 < pe ? s.a1 : dummy) + vz);     // aligned 16 B holding the tail
   s.v = ld16<kNT>(s.v_ok ? s.seg : dummy);
   const uint64_t last = s.K > 1 ? s.K - 1 : 0;
 #pragma unroll
@@ -205,7 +216,7 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
                                            uint32_t lc0, uint32_t lc1) {
   if (s.K) {
     const uint64_t K = s.K, last = K - 1;
-    if (s.ps < s.h0) reg = serial16(lds, reg, s.hc, int(s.ps - s.hbase), int(s.h0 - s.hbase));
+    if (s.ps < s.h0) reg = serial16(lds, reg, uniform4(s.hc), int(s.ps - s.hbase), int(s.h0 - s.hbase));
     uint4 v = s.v_ok ? s.v : make_uint4(0, 0, 0, 0);
     if (s.seg == s.h0) v.x ^= reg;  // the head register enters as pending word at h0
     uint32_t c0 = v.x, c1 = v.y, c2 = v.z, c3 = v.w;
@@ -272,9 +283,9 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     p = uint32_t(__builtin_amdgcn_readlane(int(p), 63));  // pending word at a1 - 4 (wave-uniform)
     reg = zmap(lds, kZ4Off, p);                              // register at a1
   } else if (s.ps < s.h0) {
-    reg = serial16(lds, reg, s.hc, int(s.ps - s.hbase), int(s.h0 - s.hbase));
+    reg = serial16(lds, reg, uniform4(s.hc), int(s.ps - s.hbase), int(s.h0 - s.hbase));
   }
-  if (s.a1 < s.pe) reg = serial16(lds, reg, s.tc, 0, int(s.pe - s.a1));
+  if (s.a1 < s.pe) reg = serial16(lds, reg, uniform4(s.tc), 0, int(s.pe - s.a1));
   return reg;
 }
 
@@ -292,6 +303,11 @@ template <bool kPlanned, bool kDynamic, int kG, bool kNT, bool kAhead, int kAbl 
 __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   const uint32_t tid = threadIdx.x;
+#ifdef KVSEP_STAMPS
+  unsigned long long e0, e1, r0, r1;
+  KVSEP_STAMP(e0);
+  KVSEP_RSTAMP(r0);
+#endif
   // ---- fill LDS: replicated Z_1024 (coalesced dword stores), then the small tables as one run
   {
     // 16-B stores: 4 consecutive dwords of the replicated image are 4 copies of one entry
@@ -308,8 +324,13 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
     for (uint32_t i = tid; i < (kLdsBytes - kZ4Off) / 16; i += kWgThreads) l128[kZ4Off / 16 + i] = src[i];
   }
   __syncthreads();
+#ifdef KVSEP_STAMPS
+  KVSEP_STAMP(e1);
+#endif
 
   const uint32_t lane = tid & 63u;
+  uint32_t vz;  // 0, opaque to the uniformity analysis (see stage())
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
   const uint32_t lc0 = (lane & 31u) << 2;
   const uint32_t lc1 = lc0 | 0x10000u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -409,7 +430,7 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
     it.only = rl(w_only) != 0;
     const uintptr_t ps = (uintptr_t(rl(uint32_t(w_ps >> 32))) << 32) | uintptr_t(rl(uint32_t(w_ps)));
     const uintptr_t pe = (uintptr_t(rl(uint32_t(w_pe >> 32))) << 32) | uintptr_t(rl(uint32_t(w_pe)));
-    stage<kG, kNT>(st, ps, pe, lane, reinterpret_cast<uintptr_t>(a.tabs));
+    stage<kG, kNT>(st, ps, pe, lane, reinterpret_cast<uintptr_t>(a.tabs), vz);
   };
   auto emit = [&](const Item& it, uint32_t reg) {
     if (lane == 0) {
@@ -418,42 +439,65 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
     }
   };
 
+  // One item: finish item g (staged in A) while item g+1 is staged into B.  The loop below alternates the
+  // roles of the two buffers (ping-pong) instead of copying B into A after each item: such a copy must wait
+  // for ALL of B's loads (vmcnt(0)) and would put a full HBM latency back on every item.
+  auto step = [&](uint64_t g, uint64_t end, Item& ia, Staged<kG>& A, Item& ib, Staged<kG>& B) {
+    const bool hn = g + 1 < end;
+#ifdef KVSEP_STAMPS  // diagnostic build only (kv-separate_amd/tools/stamp_probe.hip)
+    unsigned long long t0, t1, t2, t3;
+    KVSEP_STAMP(t0);
+#endif
+    // The next item's HBM loads overlap this item's compute.  The take is unconditional (the last item
+    // re-stages itself): on a path without it, this item's loads would be the most recent ones and the
+    // compiler's counted wait (which merges both paths) would drain everything, vmcnt(0), on every item.
+    if (kAhead) take(hn ? g + 1 : g, ib, B);
+#ifdef KVSEP_STAMPS
+    KVSEP_STAMP(t1);
+    if (hn) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // this item's 7 loads, not the next's
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    KVSEP_STAMP(t2);
+#endif
+    emit(ia, finish<kG, kNT, kAbl>(lds, A, ia.reg0, lane, lc0, lc1));
+#ifdef KVSEP_STAMPS
+    KVSEP_STAMP(t3);
+    if (lane == 0) {
+      unsigned long long* st = &g_kvsep_stamps[(uint64_t(blockIdx.x) * kWavesPerWg + wave) * 8];
+      st[0] += t1 - t0;
+      st[1] += t2 - t1;
+      st[2] += t3 - t2;
+      st[3] += 1;
+    }
+#endif
+    if (!kAhead && hn) take(g + 1, ib, B);
+    return hn;
+  };
+
   Item cur, nxt;
   Staged<kG> S, T;
   while (grab()) {
     for (uint64_t ws = lo; ws < hi; ws += 64) {
       fill(ws, hi);
+      const uint64_t end = w0 + wn;
       take(w0, cur, S);
-      for (uint64_t g = w0; g < w0 + wn; ++g) {
-        const bool hn = g + 1 < w0 + wn;
-#ifdef KVSEP_STAMPS  // diagnostic build only (kv-separate_amd/tools/stamp_probe.hip)
-        unsigned long long t0, t1, t2, t3;
-        KVSEP_STAMP(t0);
-#endif
-        if (kAhead && hn) take(g + 1, nxt, T);  // the next item's HBM loads overlap this item's compute
-#ifdef KVSEP_STAMPS
-        KVSEP_STAMP(t1);
-        if (hn) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // this item's 7 loads, not the next's
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        KVSEP_STAMP(t2);
-#endif
-        emit(cur, finish<kG, kNT, kAbl>(lds, S, cur.reg0, lane, lc0, lc1));
-#ifdef KVSEP_STAMPS
-        KVSEP_STAMP(t3);
-        if (lane == 0) {
-          unsigned long long* st = &g_kvsep_stamps[(uint64_t(blockIdx.x) * kWavesPerWg + wave) * 4];
-          st[0] += t1 - t0;
-          st[1] += t2 - t1;
-          st[2] += t3 - t2;
-          st[3] += 1;
-        }
-#endif
-        if (!kAhead && hn) take(g + 1, nxt, T);
-        cur = nxt;
-        S = T;
+      for (uint64_t g = w0;; g += 2) {
+        if (!step(g, end, cur, S, nxt, T)) break;
+        if (!step(g + 1, end, nxt, T, cur, S)) break;
       }
     }
   }
+#ifdef KVSEP_STAMPS
+  unsigned long long e2;
+  KVSEP_STAMP(e2);
+  KVSEP_RSTAMP(r1);
+  if (lane == 0) {  // [4] LDS fill cycles, [5] work-loop cycles, [6] realtime ticks (100 MHz), [7] entry cycle
+    unsigned long long* st = &g_kvsep_stamps[(uint64_t(blockIdx.x) * kWavesPerWg + wave) * 8];
+    st[4] = e1 - e0;
+    st[5] = e2 - e1;
+    st[6] = r1 - r0;
+    st[7] = r0;
+  }
+#endif
 }
 
 // One thread per block: Horner over the block's pieces, R <- Z_piece(R) ^ R_piece.

@@ -3,6 +3,8 @@
 
 usage: python ab_variants.py --variants 1,2 --configs 3a,2 --rounds 5 --steps 5
 Prints per (config, variant) the median / min kernel time and GB/s (kernel-only HIP events).
+A variant written "b<N>" runs variant N of a second build of the library (--lib-b), so two source versions
+are compared in one process on one box.
 """
 import argparse
 import os
@@ -29,11 +31,23 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--piece-kib", type=int, default=0)
+    ap.add_argument("--lib-b", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "libkvsep_b.so"))
     args = ap.parse_args()
-    variants = [int(v) for v in args.variants.split(",")]
+    variants = args.variants.split(",")
+    libs = {"a": kvsep.lib()}
+    if any(v.startswith("b") for v in variants):
+        saved = kvsep.LIB_PATH, kvsep._lib
+        kvsep.LIB_PATH, kvsep._lib = args.lib_b, None
+        libs["b"] = kvsep.lib()
+        kvsep.LIB_PATH, kvsep._lib = saved
+
+    def use(v):  # point the binding at the build variant v belongs to
+        kvsep._lib = libs["b" if v.startswith("b") else "a"]
+
     ctxs = {}
     for v in variants:
-        os.environ["KVSEP_CRC_VARIANT"] = str(v)
+        use(v)
+        os.environ["KVSEP_CRC_VARIANT"] = v.lstrip("b")
         ctxs[v] = kvsep.Context(0)
         if args.piece_kib:
             ctxs[v].set_piece_bytes(args.piece_kib * 1024)
@@ -49,11 +63,13 @@ def main():
         outs = {v: torch.zeros(off.size, dtype=torch.int32, device=dev) for v in variants}
         res = {v: [] for v in variants}
         for v in variants:
+            use(v)
             ctxs[v].reserve(off.size, useful)
             ctxs[v].batch_device(data.data_ptr(), d_off, d_len, outs[v], total_bytes=useful, max_len=int(ln.max()))
         torch.cuda.synchronize()
         for _ in range(args.rounds):
             for v in variants:
+                use(v)
                 c = ctxs[v]
                 c.set_timing(True)
                 for _ in range(args.steps):
@@ -66,7 +82,7 @@ def main():
         for v in variants:
             same = bool(torch.equal(outs[v].cpu(), ref))
             med, mn = statistics.median(res[v]), min(res[v])
-            print(f"cfg {cfg:3s} variant {v}: median {med:.4f} ms ({useful / med / 1e6:.1f} GB/s)  "
+            print(f"cfg {cfg:3s} variant {v:>3s}: median {med:.4f} ms ({useful / med / 1e6:.1f} GB/s)  "
                   f"min {mn:.4f} ms ({useful / mn / 1e6:.1f} GB/s)  same_as_v{variants[0]}={same}", flush=True)
         del data, d_off, d_len, outs
         torch.cuda.empty_cache()
