@@ -56,8 +56,9 @@ struct DevTables {
   uint32_t ztree[6][4][256];// kTreeOff   (contiguous with z4 and byte1: copied to LDS as one run)
   uint32_t byte1[256];      // kByteOff
   uint32_t zpiece[4][256];  // Z_piece_bytes, used by the combine kernel
+  uint32_t znarrow[4][256]; // Z_{16 kNarrowLanes}: the replicated table of the narrow kernel
 };
-static_assert(sizeof(DevTables) == 4096 * 9 + 1024, "table layout");
+static_assert(sizeof(DevTables) == 4096 * 10 + 1024, "table layout");
 
 struct PiecesArgs {
   const uint8_t* base;
@@ -299,6 +300,22 @@ __device__ __forceinline__ void emit_block(const PiecesArgs& a, uint64_t b, uint
   }
 }
 
+// LDS image of a CRC workgroup: the replicated fold table `rep` (4 byte-tables) at [0, 128 KiB), then the
+// small tables (Z_4, the tree tables, the byte table) as one contiguous run.
+__device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* rep, const DevTables* tabs, uint32_t tid) {
+  // 16-B stores: 4 consecutive dwords of the replicated image are 4 copies of one entry
+  uint4* l128 = reinterpret_cast<uint4*>(lds);
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) {
+    const uint32_t q = tid + i * kWgThreads;  // uint4 index in the replicated image
+    const uint32_t idx = q * 4, pair = idx >> 14, b = (idx >> 6) & 255u, half = (idx >> 5) & 1u;
+    const uint32_t v = rep[(2u * pair + half) * 256u + b];
+    l128[q] = make_uint4(v, v, v, v);
+  }
+  const uint4* src = reinterpret_cast<const uint4*>(&tabs->z4[0][0]);
+  for (uint32_t i = tid; i < (kLdsBytes - kZ4Off) / 16; i += kWgThreads) l128[kZ4Off / 16 + i] = src[i];
+}
+
 template <bool kPlanned, bool kDynamic, int kG, bool kNT, bool kAhead, int kAbl = 0>
 __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -308,21 +325,7 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
   KVSEP_STAMP(e0);
   KVSEP_RSTAMP(r0);
 #endif
-  // ---- fill LDS: replicated Z_1024 (coalesced dword stores), then the small tables as one run
-  {
-    // 16-B stores: 4 consecutive dwords of the replicated image are 4 copies of one entry
-    uint4* l128 = reinterpret_cast<uint4*>(lds);
-    const uint32_t* z = &a.tabs->z1024[0][0];
-#pragma unroll
-    for (uint32_t i = 0; i < 8; ++i) {
-      const uint32_t q = tid + i * kWgThreads;  // uint4 index in the replicated image
-      const uint32_t idx = q * 4, pair = idx >> 14, b = (idx >> 6) & 255u, half = (idx >> 5) & 1u;
-      const uint32_t v = z[(2u * pair + half) * 256u + b];
-      l128[q] = make_uint4(v, v, v, v);
-    }
-    const uint4* src = reinterpret_cast<const uint4*>(&a.tabs->z4[0][0]);
-    for (uint32_t i = tid; i < (kLdsBytes - kZ4Off) / 16; i += kWgThreads) l128[kZ4Off / 16 + i] = src[i];
-  }
+  fill_lds(lds, &a.tabs->z1024[0][0], a.tabs, tid);
   __syncthreads();
 #ifdef KVSEP_STAMPS
   KVSEP_STAMP(e1);
@@ -500,6 +503,194 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
 #endif
 }
 
+// ------------------------------------------------------------------------------------------------
+// Narrow kernel for batches of short blocks (every block <= kNarrowMax): a wavefront runs 8 blocks at once,
+// kNarrowLanes = 8 lanes ("a slot") per block and rows of 128 B ending at the block's aligned end.  The wide
+// kernel pays a fixed cost per block (lane merge, 6-level lane tree, staging: ~230 of its ~313 VALU
+// instructions for a 4 KiB block, PMC SQ_INSTS_VALU); here the merge is a 3-level tree inside the slot and
+// staging is shared by the 8 blocks, so the cost per block is mostly the fold itself.  The chain fold uses
+// the same replicated-table lookup as the wide kernel, with Z_128 (16 B per lane x 8 lanes) in place of
+// Z_1024.  All geometry is per lane (divergent across slots); every load instruction still reads whole
+// 128-B lines, one per slot.
+constexpr int kNarrowLanes = 8;
+constexpr uint32_t kNarrowRow = 16u * kNarrowLanes;
+constexpr uint64_t kNarrowMax = 64 * 1024;  // host routes a batch here when its max_len hint is <= this
+
+template <int kG>
+struct NStaged {
+  uintptr_t ps, pe, seg;  // this lane's slot item [ps, pe); its 16-B chunk of row 0
+  uint32_t K;             // body rows of the slot item
+  uint4 hc, tc, v;
+  uint4 A[kG];            // rows 1 .. kG (clamped to the last row)
+};
+
+template <int kG, bool kNT>
+__device__ __forceinline__ void nstage(NStaged<kG>& s, uintptr_t ps, uintptr_t pe, uint32_t j, uintptr_t dummy) {
+  s.ps = ps;
+  s.pe = pe;
+  const uintptr_t hbase = ps & ~uintptr_t(15);
+  uintptr_t h0 = (ps + 15) & ~uintptr_t(15);
+  if (h0 > pe) h0 = pe;
+  uintptr_t a1 = pe & ~uintptr_t(15);
+  if (a1 < h0) a1 = h0;
+  s.K = a1 > h0 ? uint32_t((a1 - h0 + kNarrowRow - 1) / kNarrowRow) : 0u;
+  s.seg = a1 - uintptr_t(s.K) * kNarrowRow + uintptr_t(j) * 16u;
+  const bool v_ok = s.K && s.seg >= h0;
+  s.hc = ld16(ps < h0 ? hbase : dummy);
+  s.tc = ld16(a1 < pe ? a1 : dummy);
+  s.v = ld16<kNT>(v_ok ? s.seg : dummy);
+  const uint32_t last = s.K > 1 ? s.K - 1 : 0;
+#pragma unroll
+  for (int i = 0; i < kG; ++i)
+    s.A[i] = ld16<kNT>(last ? s.seg + uintptr_t(1 + i < int(last) ? 1 + i : last) * kNarrowRow : dummy);
+}
+
+// Raw register after the slot item, valid in the slot's last lane (j == 7).  kmax: wave max of K.
+template <int kG, bool kNT>
+__device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, uint32_t reg, uint32_t j,
+                                            uint32_t lc0, uint32_t lc1, uint32_t kmax, uintptr_t dummy) {
+  const uintptr_t hbase = s.ps & ~uintptr_t(15);
+  uintptr_t h0 = (s.ps + 15) & ~uintptr_t(15);
+  if (h0 > s.pe) h0 = s.pe;
+  uintptr_t a1 = s.pe & ~uintptr_t(15);
+  if (a1 < h0) a1 = h0;
+  if (s.ps < h0) reg = serial16(lds, reg, s.hc, int(s.ps - hbase), int(h0 - hbase));
+  if (kmax) {
+    const uint32_t K = s.K, last = K > 1 ? K - 1 : 0;
+    uint4 v = (K && s.seg >= h0) ? s.v : make_uint4(0, 0, 0, 0);
+    if (K && s.seg == h0) v.x ^= reg;  // the head register enters as pending word at h0
+    uint32_t c0 = v.x, c1 = v.y, c2 = v.z, c3 = v.w;
+#define KVSEP_NROW(V)                          \
+  do {                                         \
+    c0 = (V).x ^ fold1024(lds, c0, lc0, lc1);  \
+    c1 = (V).y ^ fold1024(lds, c1, lc0, lc1);  \
+    c2 = (V).z ^ fold1024(lds, c2, lc0, lc1);  \
+    c3 = (V).w ^ fold1024(lds, c3, lc0, lc1);  \
+  } while (0)
+    uint32_t r = 1;
+    for (; r + kG <= kmax; r += kG) {
+      uint4 B[kG];
+      const uint32_t nr = r + kG;
+#pragma unroll
+      for (int i = 0; i < kG; ++i)
+        B[i] = ld16<kNT>(last ? s.seg + uintptr_t(nr + i < last ? nr + i : last) * kNarrowRow : dummy);
+#pragma unroll
+      for (int i = 0; i < kG; ++i)
+        if (r + i < K) KVSEP_NROW(s.A[i]);
+#pragma unroll
+      for (int i = 0; i < kG; ++i) s.A[i] = B[i];
+    }
+#pragma unroll
+    for (int i = 0; i < kG; ++i)
+      if (r + i < K) KVSEP_NROW(s.A[i]);
+#undef KVSEP_NROW
+    uint32_t p = zmap(lds, kZ4Off, c0) ^ c1;
+    p = zmap(lds, kZ4Off, p) ^ c2;
+    p = zmap(lds, kZ4Off, p) ^ c3;
+    // 3-level tree inside the slot (lanes 8k .. 8k+7 of one DPP row): Z_16, Z_32, Z_64
+    {
+      const uint32_t o = row_shr<1>(p);
+      if ((j & 1u) == 1u) p = zmap(lds, kTreeOff, o) ^ p;
+    }
+    {
+      const uint32_t o = row_shr<2>(p);
+      if ((j & 3u) == 3u) p = zmap(lds, kTreeOff + 4096u, o) ^ p;
+    }
+    {
+      const uint32_t o = row_shr<4>(p);
+      if ((j & 7u) == 7u) p = zmap(lds, kTreeOff + 8192u, o) ^ p;
+    }
+    if (K) reg = zmap(lds, kZ4Off, p);  // lane 7 of the slot: pending word at a1 - 4 -> register at a1
+  }
+  if (a1 < s.pe) reg = serial16(lds, reg, s.tc, 0, int(s.pe - a1));
+  return reg;
+}
+
+// Unsplit batches only (every block <= kNarrowMax <= piece_bytes); static contiguous runs of 8-block groups.
+template <int kG, bool kNT>
+__global__ void __launch_bounds__(kWgThreads) crc32c_narrow_kernel(PiecesArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+  const uint32_t tid = threadIdx.x;
+  fill_lds(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
+  __syncthreads();
+
+  const uint32_t lane = tid & 63u;
+  const uint32_t j = lane & (kNarrowLanes - 1);
+  const uint32_t slot = lane / kNarrowLanes;
+  const uint32_t lc0 = (lane & 31u) << 2;
+  const uint32_t lc1 = lc0 | 0x10000u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerWg;
+  const uintptr_t dummy = reinterpret_cast<uintptr_t>(a.tabs);
+  constexpr uint32_t kPerGroup = 64 / kNarrowLanes;
+
+  // contiguous run of whole groups per wave
+  const uint64_t groups = (a.count + kPerGroup - 1) / kPerGroup;
+  const uint64_t gper = (groups + nwaves - 1) / nwaves;
+  const uint64_t lo = (uint64_t(blockIdx.x) * kWavesPerWg + wave) * gper * kPerGroup;
+  uint64_t hi = lo + gper * kPerGroup;
+  if (hi > a.count) hi = a.count;
+  if (lo >= hi) return;
+
+  // descriptor window of 64 blocks (lane i <-> block w0 + i); a group's slot k reads lane (i0 + k)
+  uint64_t w0 = 0, wn = 0;
+  uintptr_t w_ps = 0, w_pe = 0;
+  uint32_t w_reg0 = 0;
+  auto fill = [&](uint64_t start, uint64_t stop) {
+    w0 = start;
+    wn = stop - start < 64 ? stop - start : 64;
+    w_ps = w_pe = dummy;
+    w_reg0 = 0;
+    if (lane < wn) {
+      const uint64_t b = start + lane;
+      const uintptr_t blk = reinterpret_cast<uintptr_t>(a.base) + a.off[b];
+      w_ps = blk;
+      w_pe = blk + a.len[b];
+      w_reg0 = ~(a.init ? a.init[b] : 0u);
+    }
+  };
+  struct NItem {
+    uint64_t b;   // per lane: block of the slot (or >= hi: empty slot)
+    uint32_t reg0;
+    uint32_t kmax;
+  };
+  auto take = [&](uint64_t g0, NItem& it, NStaged<kG>& st) {  // blocks g0 .. g0+7 of the window
+    const uint32_t src = (uint32_t(g0 - w0) + slot) * 4u;
+    auto bp = [src](uint32_t v) -> uint32_t { return uint32_t(__builtin_amdgcn_ds_bpermute(int(src), int(v))); };
+    it.b = g0 + slot;
+    it.reg0 = bp(w_reg0);
+    const uintptr_t ps = (uintptr_t(bp(uint32_t(w_ps >> 32))) << 32) | uintptr_t(bp(uint32_t(w_ps)));
+    const uintptr_t pe = (uintptr_t(bp(uint32_t(w_pe >> 32))) << 32) | uintptr_t(bp(uint32_t(w_pe)));
+    nstage<kG, kNT>(st, ps, pe, j, dummy);
+    uint32_t km = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kPerGroup; ++k) {
+      const uint32_t kk = uint32_t(__builtin_amdgcn_readlane(int(st.K), int(k * kNarrowLanes)));
+      km = km > kk ? km : kk;
+    }
+    it.kmax = km;
+  };
+  auto step = [&](uint64_t g0, uint64_t end, NItem& ia, NStaged<kG>& A, NItem& ib, NStaged<kG>& B) {
+    const bool hn = g0 + kPerGroup < end;
+    take(hn ? g0 + kPerGroup : g0, ib, B);  // unconditional: see the wide kernel's step()
+    const uint32_t reg = nfinish<kG, kNT>(lds, A, ia.reg0, j, lc0, lc1, ia.kmax, dummy);
+    if (j == kNarrowLanes - 1 && ia.b < end) emit_block(a, ia.b, ~reg);
+    return hn;
+  };
+
+  NItem cur, nxt;
+  NStaged<kG> S, T;
+  for (uint64_t ws = lo; ws < hi; ws += 64) {
+    fill(ws, hi);
+    const uint64_t end = w0 + wn;
+    take(w0, cur, S);
+    for (uint64_t g = w0;; g += 2 * kPerGroup) {
+      if (!step(g, end, cur, S, nxt, T)) break;
+      if (!step(g + kPerGroup, end, nxt, T, cur, S)) break;
+    }
+  }
+}
+
 // One thread per block: Horner over the block's pieces, R <- Z_piece(R) ^ R_piece.
 __global__ void __launch_bounds__(256) crc32c_combine_kernel(PiecesArgs a) {
   __shared__ uint32_t zp[1024];
@@ -618,6 +809,7 @@ struct kvsep_crc32c_ctx {
   int dynamic = -1;  // -1 auto, 0 static, 1 guided
   int variant = 1;   // rows per prefetch group / load policy, see launch_pieces
   uint32_t static_contig = 1;
+  int narrow = 1;    // route batches of short blocks (max_len hint <= kNarrowMax) to the narrow kernel
   Scratch sc;  // scratch of the calls made directly on this context (any stream, event-ordered)
   // timing
   bool timing = false;
@@ -654,6 +846,7 @@ int upload_tables(kvsep_crc32c_ctx* c) {
   for (int j = 0; j < 6; ++j) gf2::byte_tables(gf2::zero_bytes_map(16ull << j), &h.ztree[j][0][0]);
   for (uint32_t b = 0; b < 256; ++b) h.byte1[b] = gf2::byte_table_entry(b);
   gf2::byte_tables(gf2::zero_bytes_map(c->piece_bytes), &h.zpiece[0][0]);
+  gf2::byte_tables(gf2::zero_bytes_map(kNarrowRow), &h.znarrow[0][0]);
   if (!c->d_tabs) KVSEP_HIP(hipMalloc(&c->d_tabs, sizeof(DevTables)));
   KVSEP_HIP(hipMemcpy(c->d_tabs, &h, sizeof(DevTables), hipMemcpyHostToDevice));
   return KVSEP_OK;
@@ -819,7 +1012,11 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     e1 = take_event(c);
     if (e0 && e1) KVSEP_HIP(hipEventRecord(e0, s));
   }
-  launch_pieces(planned, dyn, c->variant, grid, s, a);
+  if (!planned && c->narrow && max_len <= kNarrowMax) {
+    crc32c_narrow_kernel<4, true><<<grid, kWgThreads, 0, s>>>(a);
+  } else {
+    launch_pieces(planned, dyn, c->variant, grid, s, a);
+  }
   KVSEP_HIP(hipGetLastError());
   if (c->timing && e0 && e1) {
     KVSEP_HIP(hipEventRecord(e1, s));
@@ -881,6 +1078,7 @@ int kvsep_crc32c_ctx_create(int device, kvsep_crc32c_ctx** out) {
   c->device = device;
   c->num_cus = prop.multiProcessorCount;
   if (const char* v = std::getenv("KVSEP_CRC_VARIANT")) c->variant = std::atoi(v);
+  if (const char* v = std::getenv("KVSEP_NARROW")) c->narrow = std::atoi(v);
   if (const char* v = std::getenv("KVSEP_CRC_STATIC_RR")) c->static_contig = std::atoi(v) ? 0 : 1;
   KVSEP_HIP(hipSetDevice(device));
   int rc = upload_tables(c);

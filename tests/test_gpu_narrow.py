@@ -1,0 +1,120 @@
+"""GPU parity of the narrow kernel (8 lanes per block, 8 blocks per wavefront), which serves every unsplit
+batch whose max_len hint is <= 64 KiB (SST blocks, WAL fragments).  Bit-exact vs the oracle restatement and
+vs the wide kernel (KVSEP_NARROW=0 context), on ragged lengths, any alignment, non-zero init, partial
+8-block groups and verify mode."""
+import os
+
+import numpy as np
+import pytest
+
+import kvsep
+from kvsep import splitmix64_bytes
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no GPU", allow_module_level=True)
+
+DEV = torch.device("cuda:0")
+NARROW_MAX = 64 * 1024
+
+
+@pytest.fixture(scope="module")
+def ctxs():
+    narrow = kvsep.Context(0)
+    old = os.environ.get("KVSEP_NARROW")
+    os.environ["KVSEP_NARROW"] = "0"
+    try:
+        wide = kvsep.Context(0)
+    finally:
+        if old is None:
+            del os.environ["KVSEP_NARROW"]
+        else:
+            os.environ["KVSEP_NARROW"] = old
+    yield narrow, wide
+    narrow.close()
+    wide.close()
+
+
+def dev_u64(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64)).to(DEV)
+
+
+def dev_u32(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32)).to(DEV)
+
+
+def run(ctx, d, off, ln, init=None, max_len=None):
+    out = torch.zeros(len(off), dtype=torch.int32, device=DEV)
+    ml = int(ln.max()) if max_len is None and len(ln) else (max_len or 0)
+    ctx.batch_device(d.data_ptr(), dev_u64(off), dev_u64(ln), out, init=None if init is None else dev_u32(init),
+                     max_len=ml, total_bytes=int(np.sum(ln, dtype=np.uint64)))
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32)
+
+
+@pytest.fixture(scope="module")
+def pool():
+    data = splitmix64_bytes(8 << 20, 1234, 0)
+    t = torch.zeros(data.size + 64, dtype=torch.uint8, device=DEV)
+    t[:data.size] = torch.from_numpy(data).to(DEV)
+    return data, t
+
+
+@pytest.mark.parametrize("count", [1, 7, 8, 9, 63, 64, 65, 1000, 4099])
+def test_ragged_any_alignment(ctxs, oracle, pool, count):
+    narrow, wide = ctxs
+    data, d = pool
+    rng = np.random.default_rng(count)
+    ln = rng.integers(0, NARROW_MAX + 1, count).astype(np.uint64)
+    short = rng.random(count) < 0.4
+    ln[short] = rng.integers(0, 300, int(short.sum()))
+    off = rng.integers(0, data.size - NARROW_MAX - 1, count).astype(np.uint64)
+    init = rng.integers(0, 2**32, count, dtype=np.uint64).astype(np.uint32)
+    exp = oracle.batch(data, off, ln, init, threads=8)
+    got = run(narrow, d, off, ln, init)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(run(wide, d, off, ln, init), exp)
+    assert np.array_equal(run(narrow, d, off, ln), oracle.batch(data, off, ln, threads=8))
+
+
+@pytest.mark.parametrize("blen", [16, 127, 128, 129, 4096, 4097, 16384, 65535, 65536])
+def test_uniform_lengths_packed(ctxs, oracle, pool, blen):
+    narrow, _ = ctxs
+    data, d = pool
+    count = min(2048, (data.size - 64) // blen)
+    for shift in (0, 1, 8, 15):
+        off = (np.arange(count, dtype=np.uint64) * np.uint64(blen) + np.uint64(shift))
+        ln = np.full(count, blen, np.uint64)
+        assert np.array_equal(run(narrow, d, off, ln), oracle.batch(data, off, ln, threads=8)), shift
+
+
+def test_mixed_slot_lengths_in_one_group(ctxs, oracle, pool):
+    """The 8 blocks of a group differ in length (divergent row counts, empty slots, head-only slots)."""
+    narrow, _ = ctxs
+    data, d = pool
+    ln = np.array([0, 1, 15, 16, 17, 65536, 4096, 3, 128, 129, 255, 0, 0, 0, 40000, 7], np.uint64)
+    off = np.array([5, 6, 7, 16, 31, 100, 4096 * 3 + 9, 1, 2, 3, 4, 5, 6, 7, 8, 9], np.uint64) * np.uint64(97)
+    init = np.arange(ln.size, dtype=np.uint32) * np.uint32(0x9E3779B1)
+    assert np.array_equal(run(narrow, d, off, ln, init), oracle.batch(data, off, ln, init, threads=4))
+
+
+def test_verify_mode_narrow(ctxs, oracle, pool):
+    narrow, _ = ctxs
+    data, d = pool
+    count = 2000  # 8,192,000 B of the 8 MiB pool
+    off = np.arange(count, dtype=np.uint64) * np.uint64(4096)
+    ln = np.full(count, 4096, np.uint64)
+    crc = oracle.batch(data, off, ln, threads=8)
+    masked = np.array([oracle.lib.oracle_crc32c_mask(int(c)) for c in crc], np.uint32)
+    for b in (17, 1500, 1999):
+        masked[b] ^= 1
+    out = torch.zeros(count, dtype=torch.int32, device=DEV)
+    fb = torch.zeros(1, dtype=torch.int64, device=DEV)
+    nb = torch.zeros(1, dtype=torch.int64, device=DEV)
+    narrow.verify_device(d.data_ptr(), dev_u64(off), dev_u64(ln), dev_u32(masked), out, fb, nb,
+                         total_bytes=int(ln.sum()), max_len=4096)
+    torch.cuda.synchronize()
+    assert fb.item() == 17 and nb.item() == 3
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), crc)
