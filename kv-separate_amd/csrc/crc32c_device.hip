@@ -103,10 +103,23 @@ __device__ __forceinline__ uint32_t lds_u32(const uint8_t* lds, uint32_t byte_of
   return *reinterpret_cast<const uint32_t*>(lds + byte_off);
 }
 
+// Three-input XOR as ONE instruction: CDNA4's v_bitop3_b32 with truth table 0x96 (a ^ b ^ c).  hipcc
+// splits a^b^c^d of four LDS results into four v_xor_b32 (interleaved with partial lgkmcnt waits), and
+// the folds are issue-bound for short blocks.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 // Z_d through a plain (non-replicated) 4 KiB table set at byte offset t.
 __device__ __forceinline__ uint32_t zmap(const uint8_t* lds, uint32_t t, uint32_t w) {
   return lds_u32(lds, t + ((w << 2) & 0x3fcu)) ^ lds_u32(lds, t + 1024u + ((w >> 6) & 0x3fcu)) ^
          lds_u32(lds, t + 2048u + ((w >> 14) & 0x3fcu)) ^ lds_u32(lds, t + 3072u + ((w >> 22) & 0x3fcu));
+}
+
+// Z_d(w) ^ x in two v_bitop3_b32.
+__device__ __forceinline__ uint32_t zmap_x(const uint8_t* lds, uint32_t t, uint32_t w, uint32_t x) {
+  return xor3(xor3(lds_u32(lds, t + ((w << 2) & 0x3fcu)), lds_u32(lds, t + 1024u + ((w >> 6) & 0x3fcu)), x),
+              lds_u32(lds, t + 2048u + ((w >> 14) & 0x3fcu)), lds_u32(lds, t + 3072u + ((w >> 22) & 0x3fcu)));
 }
 
 // Z_1024 through the replicated tables.  Layout: byte addr = pair*64K + b*256 + half*128 + copy*4
@@ -119,6 +132,15 @@ __device__ __forceinline__ uint32_t fold1024(const uint8_t* lds, uint32_t c, uin
   const uint32_t a2 = __builtin_amdgcn_perm(c, lc1, 0x0C020600u);
   const uint32_t a3 = __builtin_amdgcn_perm(c, lc1, 0x0C020700u);
   return lds_u32(lds, a0) ^ lds_u32(lds, a1 + 128u) ^ lds_u32(lds, a2) ^ lds_u32(lds, a3 + 128u);
+}
+
+// c' = w ^ Z(c) through the replicated table: two v_xor3_b32 for the five terms.
+__device__ __forceinline__ uint32_t fold_step(const uint8_t* lds, uint32_t c, uint32_t w, uint32_t lc0, uint32_t lc1) {
+  const uint32_t a0 = __builtin_amdgcn_perm(c, lc0, 0x0C020400u);
+  const uint32_t a1 = __builtin_amdgcn_perm(c, lc0, 0x0C020500u);
+  const uint32_t a2 = __builtin_amdgcn_perm(c, lc1, 0x0C020600u);
+  const uint32_t a3 = __builtin_amdgcn_perm(c, lc1, 0x0C020700u);
+  return xor3(xor3(lds_u32(lds, a0), lds_u32(lds, a1 + 128u), w), lds_u32(lds, a2), lds_u32(lds, a3 + 128u));
 }
 
 // DPP row_shr:N -- lane l receives lane l - N of its 16-lane row (a VALU op, no LDS round trip).
@@ -227,10 +249,10 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     if (kAbl == 2) {                                  \
       c0 ^= (V).x; c1 ^= (V).y; c2 ^= (V).z; c3 ^= (V).w; \
     } else {                                          \
-    c0 = (V).x ^ fold1024(lds, c0, lc0, lc1);         \
-    c1 = (V).y ^ fold1024(lds, c1, lc0, lc1);         \
-    c2 = (V).z ^ fold1024(lds, c2, lc0, lc1);         \
-    c3 = (V).w ^ fold1024(lds, c3, lc0, lc1);         \
+    c0 = fold_step(lds, c0, (V).x, lc0, lc1);         \
+    c1 = fold_step(lds, c1, (V).y, lc0, lc1);         \
+    c2 = fold_step(lds, c2, (V).z, lc0, lc1);         \
+    c3 = fold_step(lds, c3, (V).w, lc0, lc1);         \
     }                                                 \
   } while (0)
 
@@ -251,9 +273,9 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
 #undef KVSEP_ROW
     if (kAbl == 1) return c0 ^ c1 ^ c2 ^ c3 ^ lane;
     // lane merge: pending word at (16*lane + 12) of the last row
-    uint32_t p = zmap(lds, kZ4Off, c0) ^ c1;
-    p = zmap(lds, kZ4Off, p) ^ c2;
-    p = zmap(lds, kZ4Off, p) ^ c3;
+    uint32_t p = zmap_x(lds, kZ4Off, c0, c1);
+    p = zmap_x(lds, kZ4Off, p, c2);
+    p = zmap_x(lds, kZ4Off, p, c3);
     // reduction over lanes: at level j the lanes whose low j+1 bits are all ones (64 >> (j+1) of them)
     // pull the pending word of the segment 16*2^j bytes before theirs and carry it forward by 16*2^j.
     // Only those lanes touch LDS (exec-masked), which keeps the non-replicated tree tables' bank
@@ -279,7 +301,7 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
         o = uint32_t(__builtin_amdgcn_readlane(int(p), 31));
       }
       const uint32_t m = (2u << j) - 1u;
-      if ((lane & m) == m) p = zmap(lds, kTreeOff + 4096u * j, o) ^ p;
+      if ((lane & m) == m) p = zmap_x(lds, kTreeOff + 4096u * j, o, p);
     }
     p = uint32_t(__builtin_amdgcn_readlane(int(p), 63));  // pending word at a1 - 4 (wave-uniform)
     reg = zmap(lds, kZ4Off, p);                              // register at a1
@@ -305,7 +327,7 @@ __device__ __forceinline__ void emit_block(const PiecesArgs& a, uint64_t b, uint
 __device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* rep, const DevTables* tabs, uint32_t tid) {
   // 16-B stores: 4 consecutive dwords of the replicated image are 4 copies of one entry
   uint4* l128 = reinterpret_cast<uint4*>(lds);
-#pragma unroll
+#pragma unroll 2
   for (uint32_t i = 0; i < 8; ++i) {
     const uint32_t q = tid + i * kWgThreads;  // uint4 index in the replicated image
     const uint32_t idx = q * 4, pair = idx >> 14, b = (idx >> 6) & 255u, half = (idx >> 5) & 1u;
@@ -325,12 +347,6 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
   KVSEP_STAMP(e0);
   KVSEP_RSTAMP(r0);
 #endif
-  fill_lds(lds, &a.tabs->z1024[0][0], a.tabs, tid);
-  __syncthreads();
-#ifdef KVSEP_STAMPS
-  KVSEP_STAMP(e1);
-#endif
-
   const uint32_t lane = tid & 63u;
   uint32_t vz;  // 0, opaque to the uniformity analysis (see stage())
   asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
@@ -478,6 +494,11 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
 
   Item cur, nxt;
   Staged<kG> S, T;
+  fill_lds(lds, &a.tabs->z1024[0][0], a.tabs, tid);
+  __syncthreads();
+#ifdef KVSEP_STAMPS
+  KVSEP_STAMP(e1);
+#endif
   while (grab()) {
     for (uint64_t ws = lo; ws < hi; ws += 64) {
       fill(ws, hi);
@@ -562,10 +583,10 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
     uint32_t c0 = v.x, c1 = v.y, c2 = v.z, c3 = v.w;
 #define KVSEP_NROW(V)                          \
   do {                                         \
-    c0 = (V).x ^ fold1024(lds, c0, lc0, lc1);  \
-    c1 = (V).y ^ fold1024(lds, c1, lc0, lc1);  \
-    c2 = (V).z ^ fold1024(lds, c2, lc0, lc1);  \
-    c3 = (V).w ^ fold1024(lds, c3, lc0, lc1);  \
+    c0 = fold_step(lds, c0, (V).x, lc0, lc1);  \
+    c1 = fold_step(lds, c1, (V).y, lc0, lc1);  \
+    c2 = fold_step(lds, c2, (V).z, lc0, lc1);  \
+    c3 = fold_step(lds, c3, (V).w, lc0, lc1);  \
   } while (0)
     uint32_t r = 1;
     for (; r + kG <= kmax; r += kG) {
@@ -584,21 +605,21 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
     for (int i = 0; i < kG; ++i)
       if (r + i < K) KVSEP_NROW(s.A[i]);
 #undef KVSEP_NROW
-    uint32_t p = zmap(lds, kZ4Off, c0) ^ c1;
-    p = zmap(lds, kZ4Off, p) ^ c2;
-    p = zmap(lds, kZ4Off, p) ^ c3;
+    uint32_t p = zmap_x(lds, kZ4Off, c0, c1);
+    p = zmap_x(lds, kZ4Off, p, c2);
+    p = zmap_x(lds, kZ4Off, p, c3);
     // 3-level tree inside the slot (lanes 8k .. 8k+7 of one DPP row): Z_16, Z_32, Z_64
     {
       const uint32_t o = row_shr<1>(p);
-      if ((j & 1u) == 1u) p = zmap(lds, kTreeOff, o) ^ p;
+      if ((j & 1u) == 1u) p = zmap_x(lds, kTreeOff, o, p);
     }
     {
       const uint32_t o = row_shr<2>(p);
-      if ((j & 3u) == 3u) p = zmap(lds, kTreeOff + 4096u, o) ^ p;
+      if ((j & 3u) == 3u) p = zmap_x(lds, kTreeOff + 4096u, o, p);
     }
     {
       const uint32_t o = row_shr<4>(p);
-      if ((j & 7u) == 7u) p = zmap(lds, kTreeOff + 8192u, o) ^ p;
+      if ((j & 7u) == 7u) p = zmap_x(lds, kTreeOff + 8192u, o, p);
     }
     if (K) reg = zmap(lds, kZ4Off, p);  // lane 7 of the slot: pending word at a1 - 4 -> register at a1
   }
@@ -611,9 +632,6 @@ template <int kG, bool kNT>
 __global__ void __launch_bounds__(kWgThreads) crc32c_narrow_kernel(PiecesArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   const uint32_t tid = threadIdx.x;
-  fill_lds(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
-  __syncthreads();
-
   const uint32_t lane = tid & 63u;
   const uint32_t j = lane & (kNarrowLanes - 1);
   const uint32_t slot = lane / kNarrowLanes;
@@ -630,7 +648,6 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_narrow_kernel(PiecesArgs a)
   const uint64_t lo = (uint64_t(blockIdx.x) * kWavesPerWg + wave) * gper * kPerGroup;
   uint64_t hi = lo + gper * kPerGroup;
   if (hi > a.count) hi = a.count;
-  if (lo >= hi) return;
 
   // descriptor window of 64 blocks (lane i <-> block w0 + i); a group's slot k reads lane (i0 + k)
   uint64_t w0 = 0, wn = 0;
@@ -680,8 +697,11 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_narrow_kernel(PiecesArgs a)
 
   NItem cur, nxt;
   NStaged<kG> S, T;
+  if (lo < hi) fill(lo, hi);  // the first descriptor fetch overlaps the LDS fill
+  fill_lds(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
+  __syncthreads();
   for (uint64_t ws = lo; ws < hi; ws += 64) {
-    fill(ws, hi);
+    if (ws != lo) fill(ws, hi);
     const uint64_t end = w0 + wn;
     take(w0, cur, S);
     for (uint64_t g = w0;; g += 2 * kPerGroup) {
