@@ -41,8 +41,7 @@ namespace kvsep {
 
 // ------------------------------------------------------------------------------------------------
 // LDS image of one CRC workgroup (bytes).  160,768 B of the 163,840 B a gfx950 workgroup may own.
-constexpr int kWgThreads = 1024;  // 16 waves: 4 per SIMD
-constexpr int kWavesPerWg = kWgThreads / 64;
+constexpr int kWgThreads = 512;  // default CRC workgroup: 8 waves, 2 per SIMD (see launch_pieces_v)
 // [0, 128 KiB): Z_1024, 4 byte-tables x 256 entries x 32 lane copies (see fold1024)
 constexpr uint32_t kZ4Off = 131072;      // Z_4     (4 KiB)
 constexpr uint32_t kTreeOff = 135168;    // Z_16, Z_32, Z_64, Z_128, Z_256, Z_512 (6 x 4 KiB)
@@ -200,6 +199,7 @@ struct Staged {
   uint4 hc, tc;   // aligned 16 B around the head / the tail
   uint4 v;        // row 0; lanes with v_ok == false (front mask) use zeros instead
   uint4 A[kG];    // rows 1 .. kG (clamped to the last row)
+  uintptr_t dummy;  // a valid, cache-resident device address for loads whose data is never used
   bool v_ok;
 };
 
@@ -211,6 +211,7 @@ __device__ __forceinline__ void stage(Staged<kG>& s, uintptr_t ps, uintptr_t pe,
                                       uint32_t vz) {
   s.ps = ps;
   s.pe = pe;
+  s.dummy = dummy;
   s.hbase = ps & ~uintptr_t(15);
   s.h0 = (ps + 15) & ~uintptr_t(15);
   if (s.h0 > pe) s.h0 = pe;
@@ -234,9 +235,16 @@ __device__ __forceinline__ void stage(Staged<kG>& s, uintptr_t ps, uintptr_t pe,
 
 // Raw CRC register after consuming the staged item [ps, pe) from register `reg` (no final inversion).
 // Rows beyond the staged ones stream kG at a time, the next kG in flight during compute.
-template <int kG, bool kNT, int kAbl = 0>  // kAbl != 0: diagnostic ablations (wrong results)
+//
+// `next()` stages the FOLLOWING work item's loads.  It is called once, as late as possible while still ahead
+// of this item's last wait: after the last group's row loads are issued (or at once for an item with at most
+// kG rows).  So (a) the main row loop runs without the next item's 28 staged VGPRs live -- that headroom
+// lets the compiler keep all 16 LDS lookups of a row in flight instead of 2 -- and (b) the next item's
+// loads are the most recent ones, so every wait of this item stays a counted vmcnt that leaves them in
+// flight across the lane merge.
+template <int kG, bool kNT, bool kRing, int kAbl = 0, typename Next>  // kAbl != 0: diagnostic ablations (wrong results)
 __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, uint32_t reg, uint32_t lane,
-                                           uint32_t lc0, uint32_t lc1) {
+                                           uint32_t lc0, uint32_t lc1, Next&& next) {
   if (s.K) {
     const uint64_t K = s.K, last = K - 1;
     if (s.ps < s.h0) reg = serial16(lds, reg, uniform4(s.hc), int(s.ps - s.hbase), int(s.h0 - s.hbase));
@@ -255,21 +263,87 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     c3 = fold_step(lds, c3, (V).w, lc0, lc1);         \
     }                                                 \
   } while (0)
+// The group's loads go out before any of its compute: the scheduler would otherwise sink them below the
+// first row's lookups and shorten the time they are in flight (the loop is HBM-latency bound).
+#define KVSEP_LOADB(NR, CLAMP)                                                                   \
+  do {                                                                                           \
+    _Pragma("unroll") for (int i = 0; i < kG; ++i)                                               \
+      B[i] = ld16<kNT>(s.seg + (!(CLAMP) || (NR) + i < last ? (NR) + i : last) * kRowBytes);     \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+  } while (0)
 
-    uint64_t r = 1;
-    for (; r + kG <= K; r += kG) {  // full group in A: compute it while the next group loads
-      uint4 B[kG];
-      const uint64_t nr = r + kG;
+    if constexpr (kRing) {
+      // Three-slot ring of row groups (group j = rows 1+j*kG .. kG+j*kG; group 0 is the staged s.A): the
+      // group j+2 loads go out before group j is computed, so 2*kG rows stay in flight during compute
+      // (the streaming ceiling rises with rows in flight per wave, tools/hbm_probe: 4 rows 6.95 TB/s,
+      // 8 rows 7.03-7.06, 16 rows 7.08).  Unrolled by 3 so no slot is ever copied (a copy would wait for
+      // its loads); the tail runs in the same orientation with guarded rows and `dummy` loads past K.
+      const uint64_t NB = K - 1, FG = NB / kG;
+      auto gload = [&](uint4(&R)[kG], uint64_t j, bool exact) {
 #pragma unroll
-      for (int i = 0; i < kG; ++i) B[i] = ld16<kNT>(s.seg + (nr + i < last ? nr + i : last) * kRowBytes);
+        for (int i = 0; i < kG; ++i) {
+          const uint64_t row = 1 + j * kG + i;
+          R[i] = ld16<kNT>(exact || row < K ? s.seg + row * kRowBytes : s.dummy);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      auto gcomp = [&](uint4(&R)[kG], uint64_t j, bool exact) {
+#pragma unroll
+        for (int i = 0; i < kG; ++i)
+          if (exact || 1 + j * kG + i < K) KVSEP_ROW(R[i]);
+      };
+      if (NB <= kG) {  // at most one group, already staged
+        next();
+        gcomp(s.A, 0, false);
+      } else {
+        uint4 R1[kG], R2[kG];
+        gload(R1, 1, false);
+        uint64_t j = 0;
+        for (; j + 5 <= FG; j += 3) {  // groups j .. j+4 all full
+          gload(R2, j + 2, true);
+          gcomp(s.A, j, true);
+          gload(s.A, j + 3, true);
+          gcomp(R1, j + 1, true);
+          gload(R1, j + 4, true);
+          gcomp(R2, j + 2, true);
+        }
+        gload(R2, j + 2, false);
+        gcomp(s.A, j, false);
+        gload(s.A, j + 3, false);
+        gcomp(R1, j + 1, false);
+        gload(R1, j + 4, false);
+        gcomp(R2, j + 2, false);
+        next();  // after this item's last loads, and after R2 is free (no spills with 3 slots + the next item)
+        gcomp(s.A, j + 3, false);
+        gcomp(R1, j + 4, false);
+      }
+    } else {
+    uint64_t r = 1;
+    for (; r + 2 * kG <= K; r += kG) {  // full group in A, another full group after it: no next item yet
+      uint4 B[kG];
+      KVSEP_LOADB(r + kG, false);  // rows r+kG .. r+2kG-1 <= K-1: no clamp
 #pragma unroll
       for (int i = 0; i < kG; ++i) KVSEP_ROW(s.A[i]);
 #pragma unroll
       for (int i = 0; i < kG; ++i) s.A[i] = B[i];
     }
+    if (r + kG <= K) {  // the last full group: its successor rows load, then the next item stages
+      uint4 B[kG];
+      KVSEP_LOADB(r + kG, true);
+      next();
+#pragma unroll
+      for (int i = 0; i < kG; ++i) KVSEP_ROW(s.A[i]);
+#pragma unroll
+      for (int i = 0; i < kG; ++i) s.A[i] = B[i];
+      r += kG;
+    } else {
+      next();
+    }
 #pragma unroll
     for (int i = 0; i < kG; ++i)  // remainder rows r .. K-1, already in A
       if (r + i < K) KVSEP_ROW(s.A[i]);
+    }
+#undef KVSEP_LOADB
 #undef KVSEP_ROW
     if (kAbl == 1) return c0 ^ c1 ^ c2 ^ c3 ^ lane;
     // lane merge: pending word at (16*lane + 12) of the last row
@@ -305,8 +379,9 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     }
     p = uint32_t(__builtin_amdgcn_readlane(int(p), 63));  // pending word at a1 - 4 (wave-uniform)
     reg = zmap(lds, kZ4Off, p);                              // register at a1
-  } else if (s.ps < s.h0) {
-    reg = serial16(lds, reg, uniform4(s.hc), int(s.ps - s.hbase), int(s.h0 - s.hbase));
+  } else {
+    next();
+    if (s.ps < s.h0) reg = serial16(lds, reg, uniform4(s.hc), int(s.ps - s.hbase), int(s.h0 - s.hbase));
   }
   if (s.a1 < s.pe) reg = serial16(lds, reg, uniform4(s.tc), 0, int(s.pe - s.a1));
   return reg;
@@ -324,22 +399,26 @@ __device__ __forceinline__ void emit_block(const PiecesArgs& a, uint64_t b, uint
 
 // LDS image of a CRC workgroup: the replicated fold table `rep` (4 byte-tables) at [0, 128 KiB), then the
 // small tables (Z_4, the tree tables, the byte table) as one contiguous run.
+template <int kThreads = kWgThreads>
 __device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* rep, const DevTables* tabs, uint32_t tid) {
   // 16-B stores: 4 consecutive dwords of the replicated image are 4 copies of one entry
   uint4* l128 = reinterpret_cast<uint4*>(lds);
 #pragma unroll 2
-  for (uint32_t i = 0; i < 8; ++i) {
-    const uint32_t q = tid + i * kWgThreads;  // uint4 index in the replicated image
+  for (uint32_t q = tid; q < 8192; q += kThreads) {  // uint4 index in the replicated image
     const uint32_t idx = q * 4, pair = idx >> 14, b = (idx >> 6) & 255u, half = (idx >> 5) & 1u;
     const uint32_t v = rep[(2u * pair + half) * 256u + b];
     l128[q] = make_uint4(v, v, v, v);
   }
   const uint4* src = reinterpret_cast<const uint4*>(&tabs->z4[0][0]);
-  for (uint32_t i = tid; i < (kLdsBytes - kZ4Off) / 16; i += kWgThreads) l128[kZ4Off / 16 + i] = src[i];
+  for (uint32_t i = tid; i < (kLdsBytes - kZ4Off) / 16; i += kThreads) l128[kZ4Off / 16 + i] = src[i];
 }
 
-template <bool kPlanned, bool kDynamic, int kG, bool kNT, bool kAhead, int kAbl = 0>
-__global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a) {
+// kThreads: 1024 (16 waves, 4 per SIMD, <= 128 VGPRs) or 768 (12 waves, 3 per SIMD, <= 168 VGPRs: room for
+// deeper row groups).  One workgroup per CU either way (the LDS image is 157 KiB).
+template <bool kPlanned, bool kDynamic, int kG, bool kNT, bool kAhead, int kAbl = 0, bool kRing = false,
+          int kThreads = kWgThreads>
+__global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
+  constexpr uint32_t kWavesPerWg = kThreads / 64;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   const uint32_t tid = threadIdx.x;
 #ifdef KVSEP_STAMPS
@@ -467,17 +546,16 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
     unsigned long long t0, t1, t2, t3;
     KVSEP_STAMP(t0);
 #endif
-    // The next item's HBM loads overlap this item's compute.  The take is unconditional (the last item
-    // re-stages itself): on a path without it, this item's loads would be the most recent ones and the
+    // The next item's HBM loads overlap the end of this item's compute (finish() stages them late, see
+    // there).  The take is unconditional (the last item re-stages itself): on a path without it, this item's loads would be the most recent ones and the
     // compiler's counted wait (which merges both paths) would drain everything, vmcnt(0), on every item.
-    if (kAhead) take(hn ? g + 1 : g, ib, B);
 #ifdef KVSEP_STAMPS
     KVSEP_STAMP(t1);
-    if (hn) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // this item's 7 loads, not the next's
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     KVSEP_STAMP(t2);
 #endif
-    emit(ia, finish<kG, kNT, kAbl>(lds, A, ia.reg0, lane, lc0, lc1));
+    emit(ia, finish<kG, kNT, kRing, kAbl>(lds, A, ia.reg0, lane, lc0, lc1, [&]() {
+           if (kAhead) take(hn ? g + 1 : g, ib, B);
+         }));
 #ifdef KVSEP_STAMPS
     KVSEP_STAMP(t3);
     if (lane == 0) {
@@ -494,7 +572,7 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_pieces_kernel(PiecesArgs a)
 
   Item cur, nxt;
   Staged<kG> S, T;
-  fill_lds(lds, &a.tabs->z1024[0][0], a.tabs, tid);
+  fill_lds<kThreads>(lds, &a.tabs->z1024[0][0], a.tabs, tid);
   __syncthreads();
 #ifdef KVSEP_STAMPS
   KVSEP_STAMP(e1);
@@ -628,8 +706,9 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
 }
 
 // Unsplit batches only (every block <= kNarrowMax <= piece_bytes); static contiguous runs of 8-block groups.
-template <int kG, bool kNT>
-__global__ void __launch_bounds__(kWgThreads) crc32c_narrow_kernel(PiecesArgs a) {
+template <int kG, bool kNT, int kThreads>
+__global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
+  constexpr uint32_t kWavesPerWg = kThreads / 64;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
@@ -698,7 +777,7 @@ __global__ void __launch_bounds__(kWgThreads) crc32c_narrow_kernel(PiecesArgs a)
   NItem cur, nxt;
   NStaged<kG> S, T;
   if (lo < hi) fill(lo, hi);  // the first descriptor fetch overlaps the LDS fill
-  fill_lds(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
+  fill_lds<kThreads>(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
   __syncthreads();
   for (uint64_t ws = lo; ws < hi; ws += 64) {
     if (ws != lo) fill(ws, hi);
@@ -935,15 +1014,24 @@ hipEvent_t take_event(kvsep_crc32c_ctx* c) {
 
 template <bool P, bool D>
 void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs& a) {
-  // 0: 4-row groups, plain loads   1: 4-row groups, non-temporal loads, next item staged ahead
-  // 2: as 1 without staging ahead   3: 8-row groups, non-temporal, staged ahead
+  // Default (1): 8-wave workgroups (2 waves per SIMD, up to 256 VGPRs), 4-row groups, non-temporal loads, next
+  // item staged ahead.  On one MI355X, interleaved in one process (tools/ab_variants.py), 8 waves beat 16 waves
+  // by 1.5-2 % on 1 MiB blocks and by 4-5 % on the Zipf batch; 12 waves sit between.  The others are for A/B:
+  //   0: plain loads    2: no staging ahead    3: 8-row groups    4: three-slot ring of 4-row groups
+  //   5: 16-wave workgroups (the round-1 kernel)    6: 12-wave workgroups    7: 4-wave workgroups, 8-row groups
+  //   8, 9: diagnostic ablations (wrong results)
+  constexpr int T = kWgThreads;
   switch (variant) {
-    case 0: crc32c_pieces_kernel<P, D, 4, false, true><<<grid, kWgThreads, 0, s>>>(a); break;
-    case 2: crc32c_pieces_kernel<P, D, 4, true, false><<<grid, kWgThreads, 0, s>>>(a); break;
-    case 3: crc32c_pieces_kernel<P, D, 8, true, true><<<grid, kWgThreads, 0, s>>>(a); break;
-    case 8: crc32c_pieces_kernel<P, D, 4, true, true, 1><<<grid, kWgThreads, 0, s>>>(a); break;  // diag
-    case 9: crc32c_pieces_kernel<P, D, 4, true, true, 2><<<grid, kWgThreads, 0, s>>>(a); break;  // diag
-    default: crc32c_pieces_kernel<P, D, 4, true, true><<<grid, kWgThreads, 0, s>>>(a); break;
+    case 0: crc32c_pieces_kernel<P, D, 4, false, true, 0, false, T><<<grid, T, 0, s>>>(a); break;
+    case 2: crc32c_pieces_kernel<P, D, 4, true, false, 0, false, T><<<grid, T, 0, s>>>(a); break;
+    case 3: crc32c_pieces_kernel<P, D, 8, true, true, 0, false, T><<<grid, T, 0, s>>>(a); break;
+    case 4: crc32c_pieces_kernel<P, D, 4, true, true, 0, true, T><<<grid, T, 0, s>>>(a); break;
+    case 5: crc32c_pieces_kernel<P, D, 4, true, true, 0, false, 1024><<<grid, 1024, 0, s>>>(a); break;
+    case 6: crc32c_pieces_kernel<P, D, 4, true, true, 0, false, 768><<<grid, 768, 0, s>>>(a); break;
+    case 7: crc32c_pieces_kernel<P, D, 8, true, true, 0, false, 256><<<grid, 256, 0, s>>>(a); break;
+    case 8: crc32c_pieces_kernel<P, D, 4, true, true, 1, false, T><<<grid, T, 0, s>>>(a); break;  // diag
+    case 9: crc32c_pieces_kernel<P, D, 4, true, true, 2, false, T><<<grid, T, 0, s>>>(a); break;  // diag
+    default: crc32c_pieces_kernel<P, D, 4, true, true, 0, false, T><<<grid, T, 0, s>>>(a); break;
   }
 }
 
@@ -1033,7 +1121,11 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     if (e0 && e1) KVSEP_HIP(hipEventRecord(e0, s));
   }
   if (!planned && c->narrow && max_len <= kNarrowMax) {
-    crc32c_narrow_kernel<4, true><<<grid, kWgThreads, 0, s>>>(a);
+    switch (c->narrow) {  // 1: 16-wave workgroups (default); 2: 8 waves; 3: 12 waves
+      case 2: crc32c_narrow_kernel<4, true, 512><<<grid, 512, 0, s>>>(a); break;
+      case 3: crc32c_narrow_kernel<4, true, 768><<<grid, 768, 0, s>>>(a); break;
+      default: crc32c_narrow_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
+    }
   } else {
     launch_pieces(planned, dyn, c->variant, grid, s, a);
   }

@@ -4,7 +4,7 @@
 usage: python ab_variants.py --variants 1,2 --configs 3a,2 --rounds 5 --steps 5
 Prints per (config, variant) the median / min kernel time and GB/s (kernel-only HIP events).
 A variant written "b<N>" runs variant N of a second build of the library (--lib-b), so two source versions
-are compared in one process on one box.
+are compared in one process on one box; "n<K>" selects narrow-kernel variant K (KVSEP_NARROW) for short blocks.
 """
 import argparse
 import os
@@ -47,7 +47,11 @@ def main():
     ctxs = {}
     for v in variants:
         use(v)
-        os.environ["KVSEP_CRC_VARIANT"] = v.lstrip("b")
+        code = v[1:] if v.startswith("b") else v
+        if code.startswith("n"):  # "n<k>": narrow-kernel variant k (KVSEP_NARROW), default wide variant
+            os.environ["KVSEP_NARROW"], os.environ["KVSEP_CRC_VARIANT"] = code[1:], "1"
+        else:
+            os.environ["KVSEP_NARROW"], os.environ["KVSEP_CRC_VARIANT"] = "1", code
         ctxs[v] = kvsep.Context(0)
         if args.piece_kib:
             ctxs[v].set_piece_bytes(args.piece_kib * 1024)

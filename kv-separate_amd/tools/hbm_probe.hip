@@ -67,6 +67,39 @@ __global__ void k_wavechunk(const u32x4* src, size_t n16, size_t chunk16, unsign
   if (a == 0x12345678u) atomicXor(sink, a);
 }
 
+// B': as B, but the loads are inline asm with an explicit gfx950 cache policy (POL: 0 = nt, 1 = sc1 nt,
+// 2 = sc0 sc1 nt, 3 = sc0 nt), all U rows waited for at once.
+template <int POL>
+__device__ __forceinline__ u32x4 ld_pol(const u32x4* p) {
+  u32x4 v;
+  if constexpr (POL == 0) asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+  else if constexpr (POL == 1) asm volatile("global_load_dwordx4 %0, %1, off sc1 nt" : "=v"(v) : "v"(p) : "memory");
+  else if constexpr (POL == 2) asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1 nt" : "=v"(v) : "v"(p) : "memory");
+  else asm volatile("global_load_dwordx4 %0, %1, off sc0 nt" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+template <int U, int POL>
+__global__ void k_wavechunk_pol(const u32x4* src, size_t n16, size_t chunk16, unsigned* sink) {
+  const unsigned lane = threadIdx.x & 63;
+  const size_t wave = (size_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const size_t nwaves = (size_t(gridDim.x) * blockDim.x) >> 6;
+  u32x4 acc = {0, 0, 0, 0};
+  const size_t nchunks = n16 / chunk16;
+  for (size_t c = wave; c < nchunks; c += nwaves) {
+    const u32x4* p = src + c * chunk16 + lane;
+    for (size_t r = 0; r < chunk16; r += 64 * U) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = ld_pol<POL>(p + r + 64 * u);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc ^= v[u];
+    }
+  }
+  unsigned a = acc.x ^ acc.y ^ acc.z ^ acc.w;
+  if (a == 0x12345678u) atomicXor(sink, a);
+}
+
 // C: each workgroup owns a contiguous chunk; its waves interleave rows (wave w reads rows w, w+W, ...).
 template <int U, bool NT>
 __global__ void k_wgchunk(const u32x4* src, size_t n16, size_t chunk16, unsigned* sink) {
@@ -134,6 +167,28 @@ int main(int argc, char** argv) {
          size_t(CH) / 1024,                                                                              \
          timeit([&] { k_wgchunk<U, NT><<<cus * WGPERCU, BLK>>>(buf, n16, size_t(CH) / 16, sink); }, reps, \
                 double(bytes)))
+#define WP(U, POL, BLK, WGPERCU, CH)                                                                     \
+  printf("wavechunk_pol U=%d pol=%d blk=%d wg/cu=%d chunk=%zu KiB : %.1f GB/s\n", U, POL, BLK, WGPERCU,  \
+         size_t(CH) / 1024,                                                                             \
+         timeit([&] { k_wavechunk_pol<U, POL><<<cus * WGPERCU, BLK>>>(buf, n16, size_t(CH) / 16, sink); }, \
+                reps, double(bytes)))
+  if (argc > 2) {  // rows-in-flight and cache-policy sweep on 1 MiB per-wave chunks
+    WC(4, true, 1024, 1, 1 << 20);
+    WC(8, true, 1024, 1, 1 << 20);
+    WC(16, true, 1024, 1, 1 << 20);
+    WC(8, true, 512, 2, 1 << 20);
+    WC(16, true, 512, 2, 1 << 20);
+    WC(8, true, 768, 1, 1 << 20);
+    WP(8, 0, 1024, 1, 1 << 20);
+    WP(8, 1, 1024, 1, 1 << 20);
+    WP(8, 2, 1024, 1, 1 << 20);
+    WP(8, 3, 1024, 1, 1 << 20);
+    WP(16, 0, 1024, 1, 1 << 20);
+    WP(16, 2, 1024, 1, 1 << 20);
+    WC(8, true, 1024, 1, 256 << 10);
+    WC(8, false, 1024, 1, 1 << 20);
+    return 0;
+  }
   WC(4, true, 1024, 1, 4 << 10);
   WC(4, true, 1024, 1, 16 << 10);
   WC(4, true, 1024, 1, 64 << 10);
