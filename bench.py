@@ -150,7 +150,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--roundtrip-gib", type=float, default=4.0)
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    ap.add_argument("--pmc-json", default=None,
+                    help="PMC summary of the same config (default profiles/pmc_cfg<config>.json, written by "
+                         "kv-separate_amd/tools/pmc_summary.py from separate rocprofv3 --pmc passes)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -222,16 +224,18 @@ def main():
     digest = shard.crc_of_crcs(crcs, kvsep.extend_host)
     digests = shard.gather_digests(digest, dist if world > 1 else None, coll_dev)
 
-    sink = torch.zeros(4, dtype=torch.int32, device=dev)
-    ctx.stream_read(data.data_ptr(), span, sink, stream=stream)  # warm
-    torch.cuda.synchronize()
-    ctx.set_timing(True)
-    for _ in range(3):
-        ctx.stream_read(data.data_ptr(), span, sink, stream=stream)
-    torch.cuda.synchronize()
-    ctx.set_timing(False)
-    sr_ms, sr_n = ctx.get_timing()
-    read_ceiling_gbps = (span // 16 * 16) / (sr_ms / sr_n * 1e-3) / 1e9
+    read_ceiling_gbps = None  # the streaming kernel needs >= 1 MiB per wave to be a ceiling (8 GiB and up)
+    if span >= 8 * (1 << 30):
+        sink = torch.zeros(4, dtype=torch.int32, device=dev)
+        ctx.stream_read(data.data_ptr(), span, sink, stream=stream)  # warm
+        torch.cuda.synchronize()
+        ctx.set_timing(True)
+        for _ in range(3):
+            ctx.stream_read(data.data_ptr(), span, sink, stream=stream)
+        torch.cuda.synchronize()
+        ctx.set_timing(False)
+        sr_ms, sr_n = ctx.get_timing()
+        read_ceiling_gbps = (span // 16 * 16) / (sr_ms / sr_n * 1e-3) / 1e9
 
     parity = None
     cpu = None
@@ -269,6 +273,8 @@ def main():
             log(f"host round trip failed: {e}")
 
     traffic = None
+    if args.pmc_json is None:
+        args.pmc_json = os.path.join(ROOT, "profiles", f"pmc_cfg{args.config}.json")
     if os.path.exists(args.pmc_json):
         try:
             pm = json.load(open(args.pmc_json))
@@ -292,15 +298,16 @@ def main():
             "dtype": "u8",
             "data": "synthetic (splitmix64 byte stream generated in HBM)",
             "config": {"workload": desc, "config": args.config, "blocks_per_gpu": count,
-                       "bytes_per_gpu": useful, "piece_bytes": args.piece_kib * 1024 or 256 * 1024,
+                       "bytes_per_gpu": useful, "piece_bytes": args.piece_kib * 1024 or kvsep.DEFAULT_PIECE_BYTES,
                        "parallelism": f"shard{world} (independent blocks per GPU, no data-path collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved_gbps / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel": "crc32c_pieces_kernel", "kernel_avg_ms": round(kern_avg_ms, 4),
+                         "kernel": ("crc32c_narrow_kernel" if 0 < max_len <= kvsep.NARROW_MAX_LEN
+                                    else "crc32c_pieces_kernel"), "kernel_avg_ms": round(kern_avg_ms, 4),
                          "algorithmic_bytes_per_launch": useful},
             "cpu_baseline": cpu,
-            "read_ceiling_GBps": round(read_ceiling_gbps, 1),
-            "frac_of_read_ceiling": round(achieved_gbps / read_ceiling_gbps, 4),
+            "read_ceiling_GBps": read_ceiling_gbps and round(read_ceiling_gbps, 1),
+            "frac_of_read_ceiling": read_ceiling_gbps and round(achieved_gbps / read_ceiling_gbps, 4),
             "host_roundtrip_GiBps": rt,
             "host_roundtrip_parity": rt_ok,
             "parity_spot_check": parity,

@@ -54,7 +54,7 @@ typedef struct kvsep_crc32c_ctx kvsep_crc32c_ctx;
 
 int kvsep_crc32c_ctx_create(int device, kvsep_crc32c_ctx** out);
 void kvsep_crc32c_ctx_destroy(kvsep_crc32c_ctx* ctx);
-/* Work-item ("piece") size for splitting long blocks; default 256 KiB, min 1 KiB, multiple of 1 KiB. */
+/* Work-item ("piece") size for splitting long blocks; default 128 KiB, min 1 KiB, multiple of 1 KiB. */
 int kvsep_crc32c_ctx_set_piece_bytes(kvsep_crc32c_ctx* ctx, uint64_t piece_bytes);
 /* 0 = static round-robin of work items over waves, 1 = guided dynamic (one atomic per run of items),
  * -1 = auto (default): guided when long blocks are split into pieces, else static. */

@@ -242,7 +242,7 @@ __device__ __forceinline__ void stage(Staged<kG>& s, uintptr_t ps, uintptr_t pe,
 // lets the compiler keep all 16 LDS lookups of a row in flight instead of 2 -- and (b) the next item's
 // loads are the most recent ones, so every wait of this item stays a counted vmcnt that leaves them in
 // flight across the lane merge.
-template <int kG, bool kNT, bool kRing, int kAbl = 0, typename Next>  // kAbl != 0: diagnostic ablations (wrong results)
+template <int kG, bool kNT, int kAbl = 0, typename Next>  // kAbl != 0: diagnostic ablations (wrong results)
 __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, uint32_t reg, uint32_t lane,
                                            uint32_t lc0, uint32_t lc1, Next&& next) {
   if (s.K) {
@@ -272,52 +272,6 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     __builtin_amdgcn_sched_barrier(0);                                                           \
   } while (0)
 
-    if constexpr (kRing) {
-      // Three-slot ring of row groups (group j = rows 1+j*kG .. kG+j*kG; group 0 is the staged s.A): the
-      // group j+2 loads go out before group j is computed, so 2*kG rows stay in flight during compute
-      // (the streaming ceiling rises with rows in flight per wave, tools/hbm_probe: 4 rows 6.95 TB/s,
-      // 8 rows 7.03-7.06, 16 rows 7.08).  Unrolled by 3 so no slot is ever copied (a copy would wait for
-      // its loads); the tail runs in the same orientation with guarded rows and `dummy` loads past K.
-      const uint64_t NB = K - 1, FG = NB / kG;
-      auto gload = [&](uint4(&R)[kG], uint64_t j, bool exact) {
-#pragma unroll
-        for (int i = 0; i < kG; ++i) {
-          const uint64_t row = 1 + j * kG + i;
-          R[i] = ld16<kNT>(exact || row < K ? s.seg + row * kRowBytes : s.dummy);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      auto gcomp = [&](uint4(&R)[kG], uint64_t j, bool exact) {
-#pragma unroll
-        for (int i = 0; i < kG; ++i)
-          if (exact || 1 + j * kG + i < K) KVSEP_ROW(R[i]);
-      };
-      if (NB <= kG) {  // at most one group, already staged
-        next();
-        gcomp(s.A, 0, false);
-      } else {
-        uint4 R1[kG], R2[kG];
-        gload(R1, 1, false);
-        uint64_t j = 0;
-        for (; j + 5 <= FG; j += 3) {  // groups j .. j+4 all full
-          gload(R2, j + 2, true);
-          gcomp(s.A, j, true);
-          gload(s.A, j + 3, true);
-          gcomp(R1, j + 1, true);
-          gload(R1, j + 4, true);
-          gcomp(R2, j + 2, true);
-        }
-        gload(R2, j + 2, false);
-        gcomp(s.A, j, false);
-        gload(s.A, j + 3, false);
-        gcomp(R1, j + 1, false);
-        gload(R1, j + 4, false);
-        gcomp(R2, j + 2, false);
-        next();  // after this item's last loads, and after R2 is free (no spills with 3 slots + the next item)
-        gcomp(s.A, j + 3, false);
-        gcomp(R1, j + 4, false);
-      }
-    } else {
     uint64_t r = 1;
     for (; r + 2 * kG <= K; r += kG) {  // full group in A, another full group after it: no next item yet
       uint4 B[kG];
@@ -342,7 +296,6 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
 #pragma unroll
     for (int i = 0; i < kG; ++i)  // remainder rows r .. K-1, already in A
       if (r + i < K) KVSEP_ROW(s.A[i]);
-    }
 #undef KVSEP_LOADB
 #undef KVSEP_ROW
     if (kAbl == 1) return c0 ^ c1 ^ c2 ^ c3 ^ lane;
@@ -415,8 +368,7 @@ __device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* rep, cons
 
 // kThreads: 1024 (16 waves, 4 per SIMD, <= 128 VGPRs) or 768 (12 waves, 3 per SIMD, <= 168 VGPRs: room for
 // deeper row groups).  One workgroup per CU either way (the LDS image is 157 KiB).
-template <bool kPlanned, bool kDynamic, int kG, bool kNT, bool kAhead, int kAbl = 0, bool kRing = false,
-          int kThreads = kWgThreads>
+template <bool kPlanned, bool kDynamic, int kG, bool kNT, bool kAhead, int kAbl = 0, int kThreads = kWgThreads>
 __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -553,7 +505,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
     KVSEP_STAMP(t1);
     KVSEP_STAMP(t2);
 #endif
-    emit(ia, finish<kG, kNT, kRing, kAbl>(lds, A, ia.reg0, lane, lc0, lc1, [&]() {
+    emit(ia, finish<kG, kNT, kAbl>(lds, A, ia.reg0, lane, lc0, lc1, [&]() {
            if (kAhead) take(hn ? g + 1 : g, ib, B);
          }));
 #ifdef KVSEP_STAMPS
@@ -869,8 +821,11 @@ __global__ void fill_splitmix_bytes_kernel(uint8_t* dst, uint64_t n, uint64_t se
 }
 
 // The attainable-read ceiling for the same access pattern as the CRC kernel: each wave streams its own
-// contiguous 1 MiB chunk as 1 KiB rows, 8 rows in flight, non-temporal loads (hbm_probe's best pattern).
-__global__ void __launch_bounds__(1024) stream_read_kernel(uintptr_t src, uint64_t n16, uint32_t* sink) {
+// contiguous 1 MiB chunk as 1 KiB rows with non-temporal loads.  Launched as 2 x 512-thread workgroups per CU
+// with 16 rows in flight per wave: the best of tools/hbm_probe's sweep (7.08 TB/s on 64 GiB; 8 rows 7.03-7.06,
+// 4 rows 6.95).
+constexpr int kStreamRows = 16;
+__global__ void __launch_bounds__(512) stream_read_kernel(uintptr_t src, uint64_t n16, uint32_t* sink) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t wave = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = (uint64_t(gridDim.x) * blockDim.x) >> 6;
@@ -879,12 +834,13 @@ __global__ void __launch_bounds__(1024) stream_read_kernel(uintptr_t src, uint64
   uint32_t acc = 0;
   for (uint64_t c = wave; c < nchunks; c += nwaves) {
     const uintptr_t p = src + (c * kChunk16 + lane) * 16;
-    for (uint64_t r = 0; r < kChunk16 * 16; r += 8 * kRowBytes) {
-      uint4 v[8];
+    for (uint64_t r = 0; r < kChunk16 * 16; r += kStreamRows * kRowBytes) {
+      uint4 v[kStreamRows];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = ld16<true>(p + r + u * kRowBytes);
+      for (int u = 0; u < kStreamRows; ++u) v[u] = ld16<true>(p + r + u * kRowBytes);
+      __builtin_amdgcn_sched_barrier(0);  // all 16 rows in flight before any use (no register-reuse waits)
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+      for (int u = 0; u < kStreamRows; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
     }
   }
   for (uint64_t i = nchunks * kChunk16 + wave * 64 + lane; i < n16; i += nwaves * 64) {
@@ -904,7 +860,7 @@ struct kvsep_crc32c_ctx {
   int device = 0;
   int num_cus = 0;
   DevTables* d_tabs = nullptr;
-  uint64_t piece_bytes = 256 * 1024;
+  uint64_t piece_bytes = 128 * 1024;  // best of 32 KiB .. 1 MiB on configs 3a/3b/4
   int dynamic = -1;  // -1 auto, 0 static, 1 guided
   int variant = 1;   // rows per prefetch group / load policy, see launch_pieces
   uint32_t static_contig = 1;
@@ -1017,21 +973,22 @@ void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs
   // Default (1): 8-wave workgroups (2 waves per SIMD, up to 256 VGPRs), 4-row groups, non-temporal loads, next
   // item staged ahead.  On one MI355X, interleaved in one process (tools/ab_variants.py), 8 waves beat 16 waves
   // by 1.5-2 % on 1 MiB blocks and by 4-5 % on the Zipf batch; 12 waves sit between.  The others are for A/B:
-  //   0: plain loads    2: no staging ahead    3: 8-row groups    4: three-slot ring of 4-row groups
+  //   0: plain loads    2: no staging ahead    3: 8-row groups
+  // (a 3-slot ring of row groups, 8 rows in flight, and a 128-B aligned row grid that re-reads no line were
+  // both tried and measured slower: -2 to -7 % and -2 to -4 %; the extra VGPRs cost LDS-lookup overlap)
   //   5: 16-wave workgroups (the round-1 kernel)    6: 12-wave workgroups    7: 4-wave workgroups, 8-row groups
   //   8, 9: diagnostic ablations (wrong results)
   constexpr int T = kWgThreads;
   switch (variant) {
-    case 0: crc32c_pieces_kernel<P, D, 4, false, true, 0, false, T><<<grid, T, 0, s>>>(a); break;
-    case 2: crc32c_pieces_kernel<P, D, 4, true, false, 0, false, T><<<grid, T, 0, s>>>(a); break;
-    case 3: crc32c_pieces_kernel<P, D, 8, true, true, 0, false, T><<<grid, T, 0, s>>>(a); break;
-    case 4: crc32c_pieces_kernel<P, D, 4, true, true, 0, true, T><<<grid, T, 0, s>>>(a); break;
-    case 5: crc32c_pieces_kernel<P, D, 4, true, true, 0, false, 1024><<<grid, 1024, 0, s>>>(a); break;
-    case 6: crc32c_pieces_kernel<P, D, 4, true, true, 0, false, 768><<<grid, 768, 0, s>>>(a); break;
-    case 7: crc32c_pieces_kernel<P, D, 8, true, true, 0, false, 256><<<grid, 256, 0, s>>>(a); break;
-    case 8: crc32c_pieces_kernel<P, D, 4, true, true, 1, false, T><<<grid, T, 0, s>>>(a); break;  // diag
-    case 9: crc32c_pieces_kernel<P, D, 4, true, true, 2, false, T><<<grid, T, 0, s>>>(a); break;  // diag
-    default: crc32c_pieces_kernel<P, D, 4, true, true, 0, false, T><<<grid, T, 0, s>>>(a); break;
+    case 0: crc32c_pieces_kernel<P, D, 4, false, true, 0, T><<<grid, T, 0, s>>>(a); break;
+    case 2: crc32c_pieces_kernel<P, D, 4, true, false, 0, T><<<grid, T, 0, s>>>(a); break;
+    case 3: crc32c_pieces_kernel<P, D, 8, true, true, 0, T><<<grid, T, 0, s>>>(a); break;
+    case 5: crc32c_pieces_kernel<P, D, 4, true, true, 0, 1024><<<grid, 1024, 0, s>>>(a); break;
+    case 6: crc32c_pieces_kernel<P, D, 4, true, true, 0, 768><<<grid, 768, 0, s>>>(a); break;
+    case 7: crc32c_pieces_kernel<P, D, 8, true, true, 0, 256><<<grid, 256, 0, s>>>(a); break;
+    case 8: crc32c_pieces_kernel<P, D, 4, true, true, 1, T><<<grid, T, 0, s>>>(a); break;  // diag
+    case 9: crc32c_pieces_kernel<P, D, 4, true, true, 2, T><<<grid, T, 0, s>>>(a); break;  // diag
+    default: crc32c_pieces_kernel<P, D, 4, true, true, 0, T><<<grid, T, 0, s>>>(a); break;
   }
 }
 
@@ -1361,7 +1318,7 @@ int kvsep_stream_read_device(kvsep_crc32c_ctx* c, void* stream, const void* src,
     e1 = take_event(c);
     if (e0 && e1) KVSEP_HIP(hipEventRecord(e0, s));
   }
-  stream_read_kernel<<<unsigned(c->num_cus), 1024, 0, s>>>(reinterpret_cast<uintptr_t>(src), n16, sink);
+  stream_read_kernel<<<unsigned(2 * c->num_cus), 512, 0, s>>>(reinterpret_cast<uintptr_t>(src), n16, sink);
   KVSEP_HIP(hipGetLastError());
   if (c->timing && e0 && e1) {
     KVSEP_HIP(hipEventRecord(e1, s));

@@ -185,6 +185,10 @@ def _dptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+DEFAULT_PIECE_BYTES = 128 * 1024  # the library default (kvsep_crc32c_ctx, crc32c_device.hip)
+NARROW_MAX_LEN = 64 * 1024  # batches whose max_len hint is <= this run the narrow kernel (kNarrowMax)
+
+
 class Context:
     """One per device: uploads the Z_d tables once, owns scratch and staging."""
 

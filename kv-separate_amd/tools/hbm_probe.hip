@@ -120,6 +120,16 @@ __global__ void k_wgchunk(const u32x4* src, size_t n16, size_t chunk16, unsigned
   if (a == 0x12345678u) atomicXor(sink, a);
 }
 
+__global__ void k_fill_random(u32x4* dst, size_t n16) {
+  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n16; i += size_t(gridDim.x) * blockDim.x) {
+    uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    dst[i] = u32x4{unsigned(z), unsigned(z >> 32), unsigned(z * 3), unsigned((z * 3) >> 32)};
+  }
+}
+
 template <typename F>
 double timeit(F f, int reps, double bytes) {
   hipEvent_t a, b;
@@ -172,6 +182,20 @@ int main(int argc, char** argv) {
          size_t(CH) / 1024,                                                                             \
          timeit([&] { k_wavechunk_pol<U, POL><<<cus * WGPERCU, BLK>>>(buf, n16, size_t(CH) / 16, sink); }, \
                 reps, double(bytes)))
+  if (argc > 2 && argv[2][0] == 'r') {  // constant vs random data, chunk size, at the best rows-in-flight
+    WC(16, true, 512, 2, 1 << 20);
+    WC(16, true, 512, 2, 128 << 10);
+    WC(8, true, 512, 1, 128 << 10);
+    k_fill_random<<<cus * 8, 256>>>(buf, n16);
+    CHECK(hipDeviceSynchronize());
+    printf("random data:\n");
+    WC(16, true, 512, 2, 1 << 20);
+    WC(16, true, 512, 2, 128 << 10);
+    WC(8, true, 512, 1, 128 << 10);
+    WC(4, true, 512, 1, 128 << 10);
+    WC(8, true, 1024, 1, 1 << 20);
+    return 0;
+  }
   if (argc > 2) {  // rows-in-flight and cache-policy sweep on 1 MiB per-wave chunks
     WC(4, true, 1024, 1, 1 << 20);
     WC(8, true, 1024, 1, 1 << 20);

@@ -62,7 +62,7 @@ def test_sweep_every_offset_and_length(ctx, golden, piece, dynamic):
     for max_len in (0, 256):
         assert np.array_equal(run(ctx, d, off, ln, max_len=max_len), exp0)
         assert np.array_equal(run(ctx, d, off, ln, init, max_len=max_len), expi)
-    ctx.set_piece_bytes(256 * 1024)
+    ctx.set_piece_bytes(kvsep.DEFAULT_PIECE_BYTES)
     ctx.set_schedule(None)
 
 
@@ -77,7 +77,7 @@ def test_large_blocks_golden(ctx, golden, piece):
     exp = np.array([c["crc"] for c in cases], np.uint32)
     assert np.array_equal(run(ctx, d, off, ln, init), exp)
     assert np.array_equal(run(ctx, d, off, ln, init, max_len=int(ln.max())), exp)
-    ctx.set_piece_bytes(256 * 1024)
+    ctx.set_piece_bytes(kvsep.DEFAULT_PIECE_BYTES)
 
 
 def test_known_vectors(ctx, golden):
@@ -148,7 +148,7 @@ def test_cfg4_ragged_sample_vs_oracle(ctx, oracle):
         for dyn in (True, False):
             ctx.set_schedule(dyn)
             assert np.array_equal(run(ctx, d, off, ln), exp), (piece, dyn)
-    ctx.set_piece_bytes(256 * 1024)
+    ctx.set_piece_bytes(kvsep.DEFAULT_PIECE_BYTES)
     ctx.set_schedule(None)
 
 
@@ -165,7 +165,7 @@ def test_random_blocks_many_pieces_vs_oracle(ctx, oracle):
     for piece in (1024, 3072, 8192, 256 * 1024):
         ctx.set_piece_bytes(piece)
         assert np.array_equal(run(ctx, d, off, ln, init), exp), piece
-    ctx.set_piece_bytes(256 * 1024)
+    ctx.set_piece_bytes(kvsep.DEFAULT_PIECE_BYTES)
 
 
 def test_edge_cases(ctx):
