@@ -354,16 +354,37 @@ __device__ __forceinline__ void emit_block(const PiecesArgs& a, uint64_t b, uint
 // small tables (Z_4, the tree tables, the byte table) as one contiguous run.
 template <int kThreads = kWgThreads>
 __device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* rep, const DevTables* tabs, uint32_t tid) {
-  // 16-B stores: 4 consecutive dwords of the replicated image are 4 copies of one entry
+  // Every global load of the fill is issued before the first LDS store: one L2/HBM round trip per
+  // workgroup instead of one per loop trip (the fill is a fixed cost of every launch; it dominates
+  // small batches, e.g. 4 KiB-block batches of a few MiB).
+  constexpr uint32_t kRep = (8192 + kThreads - 1) / kThreads;                           // uint4 stores
+  constexpr uint32_t kSmall = ((kLdsBytes - kZ4Off) / 16 + kThreads - 1) / kThreads;  // uint4 copies
   uint4* l128 = reinterpret_cast<uint4*>(lds);
-#pragma unroll 2
-  for (uint32_t q = tid; q < 8192; q += kThreads) {  // uint4 index in the replicated image
-    const uint32_t idx = q * 4, pair = idx >> 14, b = (idx >> 6) & 255u, half = (idx >> 5) & 1u;
-    const uint32_t v = rep[(2u * pair + half) * 256u + b];
-    l128[q] = make_uint4(v, v, v, v);
-  }
   const uint4* src = reinterpret_cast<const uint4*>(&tabs->z4[0][0]);
-  for (uint32_t i = tid; i < (kLdsBytes - kZ4Off) / 16; i += kThreads) l128[kZ4Off / 16 + i] = src[i];
+  uint32_t v[kRep];
+  uint4 w[kSmall];
+#pragma unroll
+  for (uint32_t i = 0; i < kRep; ++i) {
+    const uint32_t q = tid + i * kThreads;  // uint4 index in the replicated image
+    const uint32_t idx = q * 4, pair = idx >> 14, b = (idx >> 6) & 255u, half = (idx >> 5) & 1u;
+    v[i] = q < 8192 ? rep[(2u * pair + half) * 256u + b] : 0u;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kSmall; ++i) {
+    const uint32_t q = tid + i * kThreads;
+    w[i] = q < (kLdsBytes - kZ4Off) / 16 ? src[q] : make_uint4(0, 0, 0, 0);
+  }
+  // 16-B stores: 4 consecutive dwords of the replicated image are 4 copies of one entry
+#pragma unroll
+  for (uint32_t i = 0; i < kRep; ++i) {
+    const uint32_t q = tid + i * kThreads;
+    if (q < 8192) l128[q] = make_uint4(v[i], v[i], v[i], v[i]);
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kSmall; ++i) {
+    const uint32_t q = tid + i * kThreads;
+    if (q < (kLdsBytes - kZ4Off) / 16) l128[kZ4Off / 16 + q] = w[i];
+  }
 }
 
 // kThreads: 1024 (16 waves, 4 per SIMD, <= 128 VGPRs) or 768 (12 waves, 3 per SIMD, <= 168 VGPRs: room for
@@ -596,15 +617,18 @@ __device__ __forceinline__ void nstage(NStaged<kG>& s, uintptr_t ps, uintptr_t p
     s.A[i] = ld16<kNT>(last ? s.seg + uintptr_t(1 + i < int(last) ? 1 + i : last) * kNarrowRow : dummy);
 }
 
-// Raw register after the slot item, valid in the slot's last lane (j == 7).  kmax: wave max of K.
-template <int kG, bool kNT>
+// Raw register after the slot item, valid in the slot's last lane (j == 7).  kmin / kmax: wave min / max of K.
+// `next()` stages the following group, after this group's last row loads (see the wide kernel's finish()).
+template <int kG, bool kNT, typename Next>
 __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, uint32_t reg, uint32_t j,
-                                            uint32_t lc0, uint32_t lc1, uint32_t kmax, uintptr_t dummy) {
+                                            uint32_t lc0, uint32_t lc1, uint32_t kmin, uint32_t kmax,
+                                            uintptr_t dummy, Next&& next) {
   const uintptr_t hbase = s.ps & ~uintptr_t(15);
   uintptr_t h0 = (s.ps + 15) & ~uintptr_t(15);
   if (h0 > s.pe) h0 = s.pe;
   uintptr_t a1 = s.pe & ~uintptr_t(15);
   if (a1 < h0) a1 = h0;
+  if (!kmax) next();
   if (s.ps < h0) reg = serial16(lds, reg, s.hc, int(s.ps - hbase), int(h0 - hbase));
   if (kmax) {
     const uint32_t K = s.K, last = K > 1 ? K - 1 : 0;
@@ -619,18 +643,30 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
     c3 = fold_step(lds, c3, (V).w, lc0, lc1);  \
   } while (0)
     uint32_t r = 1;
-    for (; r + kG <= kmax; r += kG) {
+    for (; r + 2 * kG <= kmin; r += kG) {  // every slot has rows r .. r+2kG-1: no guards, no clamps
+      uint4 B[kG];
+#pragma unroll
+      for (int i = 0; i < kG; ++i) B[i] = ld16<kNT>(s.seg + uintptr_t(r + kG + i) * kNarrowRow);
+      __builtin_amdgcn_sched_barrier(0);  // loads go out before the group's compute
+#pragma unroll
+      for (int i = 0; i < kG; ++i) KVSEP_NROW(s.A[i]);
+#pragma unroll
+      for (int i = 0; i < kG; ++i) s.A[i] = B[i];
+    }
+    for (; r + kG <= kmax; r += kG) {  // ragged end: per-lane clamps and guards
       uint4 B[kG];
       const uint32_t nr = r + kG;
 #pragma unroll
       for (int i = 0; i < kG; ++i)
         B[i] = ld16<kNT>(last ? s.seg + uintptr_t(nr + i < last ? nr + i : last) * kNarrowRow : dummy);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < kG; ++i)
         if (r + i < K) KVSEP_NROW(s.A[i]);
 #pragma unroll
       for (int i = 0; i < kG; ++i) s.A[i] = B[i];
     }
+    next();
 #pragma unroll
     for (int i = 0; i < kG; ++i)
       if (r + i < K) KVSEP_NROW(s.A[i]);
@@ -700,7 +736,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   struct NItem {
     uint64_t b;   // per lane: block of the slot (or >= hi: empty slot)
     uint32_t reg0;
-    uint32_t kmax;
+    uint32_t kmin, kmax;
   };
   auto take = [&](uint64_t g0, NItem& it, NStaged<kG>& st) {  // blocks g0 .. g0+7 of the window
     const uint32_t src = (uint32_t(g0 - w0) + slot) * 4u;
@@ -710,18 +746,21 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     const uintptr_t ps = (uintptr_t(bp(uint32_t(w_ps >> 32))) << 32) | uintptr_t(bp(uint32_t(w_ps)));
     const uintptr_t pe = (uintptr_t(bp(uint32_t(w_pe >> 32))) << 32) | uintptr_t(bp(uint32_t(w_pe)));
     nstage<kG, kNT>(st, ps, pe, j, dummy);
-    uint32_t km = 0;
+    uint32_t km = 0, kn = ~0u;
 #pragma unroll
     for (uint32_t k = 0; k < kPerGroup; ++k) {
       const uint32_t kk = uint32_t(__builtin_amdgcn_readlane(int(st.K), int(k * kNarrowLanes)));
       km = km > kk ? km : kk;
+      kn = kn < kk ? kn : kk;
     }
     it.kmax = km;
+    it.kmin = kn;
   };
   auto step = [&](uint64_t g0, uint64_t end, NItem& ia, NStaged<kG>& A, NItem& ib, NStaged<kG>& B) {
     const bool hn = g0 + kPerGroup < end;
-    take(hn ? g0 + kPerGroup : g0, ib, B);  // unconditional: see the wide kernel's step()
-    const uint32_t reg = nfinish<kG, kNT>(lds, A, ia.reg0, j, lc0, lc1, ia.kmax, dummy);
+    // next group staged inside nfinish, after this group's last row loads; unconditional (see the wide step())
+    const uint32_t reg = nfinish<kG, kNT>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
+                                          [&]() { take(hn ? g0 + kPerGroup : g0, ib, B); });
     if (j == kNarrowLanes - 1 && ia.b < end) emit_block(a, ia.b, ~reg);
     return hn;
   };

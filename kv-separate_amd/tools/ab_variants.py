@@ -20,6 +20,9 @@ from kvsep import workloads as W  # noqa: E402
 
 
 def layout(cfg):
+    if cfg.startswith("u"):  # "u<count>x<len>": uniform packed blocks, e.g. u4096x4096
+        count, length = cfg[1:].split("x")
+        return W.uniform_layout(int(count), int(length))
     return {"3a": W.cfg3_layout, "3b": lambda: W.cfg3_layout(vlog=True), "2": W.cfg2_layout,
             "4": W.cfg4_layout}[cfg]()
 
