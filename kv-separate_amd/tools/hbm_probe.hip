@@ -53,6 +53,7 @@ __global__ void k_wavechunk(const u32x4* src, size_t n16, size_t chunk16, unsign
   const size_t nwaves = (size_t(gridDim.x) * blockDim.x) >> 6;
   u32x4 acc = {0, 0, 0, 0};
   const size_t nchunks = n16 / chunk16;
+  if (chunk16 % (64 * U)) return;  // whole U-row steps only (else reads overrun the buffer)
   for (size_t c = wave; c < nchunks; c += nwaves) {
     const u32x4* p = src + c * chunk16 + lane;
     for (size_t r = 0; r < chunk16; r += 64 * U) {
@@ -85,6 +86,7 @@ __global__ void k_wavechunk_pol(const u32x4* src, size_t n16, size_t chunk16, un
   const size_t nwaves = (size_t(gridDim.x) * blockDim.x) >> 6;
   u32x4 acc = {0, 0, 0, 0};
   const size_t nchunks = n16 / chunk16;
+  if (chunk16 % (64 * U)) return;
   for (size_t c = wave; c < nchunks; c += nwaves) {
     const u32x4* p = src + c * chunk16 + lane;
     for (size_t r = 0; r < chunk16; r += 64 * U) {
@@ -106,6 +108,7 @@ __global__ void k_wgchunk(const u32x4* src, size_t n16, size_t chunk16, unsigned
   const unsigned lane = threadIdx.x & 63, w = threadIdx.x >> 6, W = blockDim.x >> 6;
   u32x4 acc = {0, 0, 0, 0};
   const size_t nchunks = n16 / chunk16;
+  if (chunk16 % (size_t(64) * W * U)) return;  // a chunk must hold whole U-row steps (else reads overrun the buffer)
   for (size_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
     const u32x4* p = src + c * chunk16 + lane + 64 * w;
     for (size_t r = 0; r < chunk16; r += size_t(64) * W * U) {
@@ -221,7 +224,7 @@ int main(int argc, char** argv) {
   WC(4, true, 256, 8, 4 << 10);
   WC(4, true, 512, 4, 4 << 10);
   WG(4, true, 1024, 1, 64 << 10);
-  WG(4, true, 1024, 1, 16 << 10);
+  WG(4, true, 1024, 1, 256 << 10);
   WG(1, true, 1024, 1, 16 << 10);
   GS(4, true, 256, 8);
   return 0;
