@@ -142,7 +142,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="3a", choices=["3a", "3b", "2", "4"])
+    ap.add_argument("--config", default="3a", choices=["3a", "3b", "2", "4", "5"],
+                    help="BASELINE.json config; 5 = the 512 GiB vlog batch split over the ranks (strong scaling)")
     ap.add_argument("--piece-kib", type=int, default=0, help="work-item size (0 = library default)")
     ap.add_argument("--schedule", default="default", choices=["default", "static", "dynamic"])
     ap.add_argument("--no-plan-hint", action="store_true", help="pass max_len = 0 (force the planning pass)")
@@ -176,7 +177,20 @@ def main():
     if args.schedule != "default":
         ctx.set_schedule(args.schedule == "dynamic")
 
-    off, ln, desc = layout(args.config)
+    passes = 1
+    if args.config == "5":
+        # Config 5: ONE 512 GiB vlog batch (524,288 records of 1,048,609 B, variant-B framing) split over the
+        # ranks.  512 GiB exceeds one GPU's HBM, so each rank keeps a 64 GiB slice of records resident and a
+        # step runs 8/N passes over it (each pass reads all 64 GiB from HBM again; nothing is cached at
+        # this size).  Total work per step is fixed: strong scaling.
+        if 8 % world:
+            raise SystemExit("--config 5 needs 1, 2, 4 or 8 ranks")
+        passes = 8 // world
+        off, ln, _ = layout("3b")
+        desc = (f"512 GiB vlog batch (524,288 x 1,048,609-B records) over {world} GPU(s): {passes} pass(es) "
+                f"of a resident 64 GiB slice per GPU (config 5)")
+    else:
+        off, ln, desc = layout(args.config)
     count = int(off.size)
     useful = int(ln.sum())
     span = int(off[-1] + ln[-1])
@@ -185,7 +199,7 @@ def main():
 
     # synthetic data, generated in HBM: rank r holds bytes [r*span, (r+1)*span) of one stream
     data = torch.empty(span + 64, dtype=torch.uint8, device=dev)
-    seed = W.SEED + (1 if args.config.startswith("3") else 2 if args.config == "4" else 0)
+    seed = W.SEED + (1 if args.config[0] in "35" else 2 if args.config == "4" else 0)
     kvsep.fill_splitmix64(data.data_ptr(), span, seed, shard.stream_offset(rank, span))
     d_off, d_len = to_dev_u64(off, dev), to_dev_u64(ln, dev)
     out = torch.zeros(count, dtype=torch.int32, device=dev)
@@ -193,8 +207,9 @@ def main():
     stream = torch.cuda.current_stream()
 
     def step():
-        ctx.batch_device(data.data_ptr(), d_off, d_len, out, count=count, total_bytes=useful, max_len=max_len,
-                         stream=stream)
+        for _ in range(passes):
+            ctx.batch_device(data.data_ptr(), d_off, d_len, out, count=count, total_bytes=useful, max_len=max_len,
+                             stream=stream)
 
     for _ in range(args.warmup):
         step()
@@ -215,7 +230,7 @@ def main():
     kern_ms, launches = ctx.get_timing()
     elapsed = shard.max_over_ranks(elapsed, dist if world > 1 else None, coll_dev)
     ms_per_step = elapsed * 1e3 / args.steps
-    value = world * useful * args.steps / GIB / elapsed
+    value = world * passes * useful * args.steps / GIB / elapsed
     kern_avg_ms = kern_ms / max(1, launches)
     achieved_gbps = useful / (kern_avg_ms * 1e-3) / 1e9
 
@@ -273,12 +288,13 @@ def main():
             log(f"host round trip failed: {e}")
 
     traffic = None
+    pmc_cfg = "3b" if args.config == "5" else args.config  # config 5's launches are config-3b launches
     if args.pmc_json is None:
-        args.pmc_json = os.path.join(ROOT, "profiles", f"pmc_cfg{args.config}.json")
+        args.pmc_json = os.path.join(ROOT, "profiles", f"pmc_cfg{pmc_cfg}.json")
     if os.path.exists(args.pmc_json):
         try:
             pm = json.load(open(args.pmc_json))
-            if pm.get("config") == args.config:
+            if pm.get("config") == pmc_cfg:
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -293,12 +309,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.config == "5" else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 byte stream generated in HBM)",
-            "config": {"workload": desc, "config": args.config, "blocks_per_gpu": count,
-                       "bytes_per_gpu": useful, "piece_bytes": args.piece_kib * 1024 or kvsep.DEFAULT_PIECE_BYTES,
+            "config": {"workload": desc, "config": args.config, "blocks_per_gpu": count * passes,
+                       "bytes_per_gpu": useful * passes, "piece_bytes": args.piece_kib * 1024 or kvsep.DEFAULT_PIECE_BYTES,
                        "parallelism": f"shard{world} (independent blocks per GPU, no data-path collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved_gbps / HBM_PEAK_GBPS, 4), "traffic": traffic,
