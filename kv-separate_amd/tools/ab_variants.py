@@ -4,7 +4,8 @@
 usage: python ab_variants.py --variants 1,2 --configs 3a,2 --rounds 5 --steps 5
 Prints per (config, variant) the median / min kernel time and GB/s (kernel-only HIP events).
 A variant written "b<N>" runs variant N of a second build of the library (--lib-b), so two source versions
-are compared in one process on one box; "n<K>" selects narrow-kernel variant K (KVSEP_NARROW) for short blocks.
+are compared in one process on one box; "n<K>" selects narrow-kernel variant K (KVSEP_NARROW) for short blocks;
+"<N>p<KiB>" runs variant N with its own piece size.
 """
 import argparse
 import os
@@ -51,13 +52,17 @@ def main():
     for v in variants:
         use(v)
         code = v[1:] if v.startswith("b") else v
+        piece_kib = args.piece_kib
+        if "p" in code:  # "<variant>p<KiB>": that variant with its own piece size, e.g. 1p128 vs 1p1024
+            code, pk = code.split("p")
+            piece_kib = int(pk)
         if code.startswith("n"):  # "n<k>": narrow-kernel variant k (KVSEP_NARROW), default wide variant
             os.environ["KVSEP_NARROW"], os.environ["KVSEP_CRC_VARIANT"] = code[1:], "1"
         else:
             os.environ["KVSEP_NARROW"], os.environ["KVSEP_CRC_VARIANT"] = "1", code
         ctxs[v] = kvsep.Context(0)
-        if args.piece_kib:
-            ctxs[v].set_piece_bytes(args.piece_kib * 1024)
+        if piece_kib:
+            ctxs[v].set_piece_bytes(piece_kib * 1024)
     dev = torch.device("cuda:0")
     for cfg in args.configs.split(","):
         off, ln = layout(cfg)

@@ -197,6 +197,15 @@ int main(int argc, char** argv) {
     WC(8, true, 512, 1, 128 << 10);
     WC(4, true, 512, 1, 128 << 10);
     WC(8, true, 1024, 1, 1 << 20);
+    WG(16, true, 512, 2, 1 << 20);
+    WG(8, true, 512, 2, 1 << 20);
+    WG(4, true, 512, 1, 1 << 20);
+    WG(8, true, 512, 1, 1 << 20);
+    WG(8, true, 512, 1, 128 << 10);
+    WG(4, true, 512, 1, 128 << 10);
+    WG(2, true, 512, 1, 1 << 20);
+    WG(8, true, 1024, 1, 1 << 20);
+    WG(4, true, 1024, 1, 1 << 20);
     return 0;
   }
   if (argc > 2) {  // rows-in-flight and cache-policy sweep on 1 MiB per-wave chunks
