@@ -46,6 +46,10 @@ uint32_t kvsep_crc32c_unmask(uint32_t masked_crc);       /* util/crc32c.h:35-38 
 /* port/port_stdcxx.h:142: returns Extend(crc, buf, size); never 0 for the self-test buffer. */
 uint32_t kvsep_accelerated_crc32c(uint32_t crc, const char* buf, size_t size);
 void kvsep_set_offload_threshold(uint64_t nbytes);
+/* Counters of the scalar drop-in since load (any may be null): calls served by the GPU, calls served by
+ * the host path below the threshold, and calls at/above the threshold that the GPU could not serve and
+ * that finished on the host (set KVSEP_STRICT_GPU=1 to abort on those instead). */
+void kvsep_offload_stats(uint64_t* gpu_calls, uint64_t* host_calls, uint64_t* gpu_failures);
 /* Host-only CRC (SSE4.2 crc32 instructions, 3-way interleaved): the small-input leg of Extend. */
 uint32_t kvsep_crc32c_extend_host(uint32_t init_crc, const char* data, size_t n);
 

@@ -37,6 +37,7 @@ void release_staging(HostStaging& s) {
 namespace {
 
 std::atomic<uint64_t> g_offload_threshold{64ull << 20};
+std::atomic<uint64_t> g_gpu_calls{0}, g_host_calls{0}, g_gpu_failures{0};
 
 // ------------------------------------------------------------------ host CRC (SSE4.2)
 // The crc32 instruction implements exactly the reflected Castagnoli register update of
@@ -265,11 +266,17 @@ uint32_t kvsep_crc32c_extend(uint32_t init_crc, const char* data, size_t n) {
     if (c) {
       const uint64_t off = 0, len = n;
       uint32_t out = 0;
-      if (kvsep_crc32c_batch_host_span(c, data, n, &off, &len, &init_crc, &out, 1) == KVSEP_OK) return out;
+      if (kvsep_crc32c_batch_host_span(c, data, n, &off, &len, &init_crc, &out, 1) == KVSEP_OK) {
+        g_gpu_calls.fetch_add(1, std::memory_order_relaxed);
+        return out;
+      }
       std::fprintf(stderr, "kvsep_crc32c: GPU offload failed: %s\n", kvsep_last_error());
     }
     // Extend is total (util/crc32c.h:17 has no error channel): a strict deployment aborts instead.
     if (std::getenv("KVSEP_STRICT_GPU")) std::abort();
+    g_gpu_failures.fetch_add(1, std::memory_order_relaxed);
+  } else {
+    g_host_calls.fetch_add(1, std::memory_order_relaxed);
   }
   return host_crc(init_crc, reinterpret_cast<const uint8_t*>(data), n);
 }
@@ -288,6 +295,12 @@ uint32_t kvsep_accelerated_crc32c(uint32_t crc, const char* buf, size_t size) {
 }
 
 void kvsep_set_offload_threshold(uint64_t nbytes) { g_offload_threshold.store(nbytes); }
+
+void kvsep_offload_stats(uint64_t* gpu_calls, uint64_t* host_calls, uint64_t* gpu_failures) {
+  if (gpu_calls) *gpu_calls = g_gpu_calls.load();
+  if (host_calls) *host_calls = g_host_calls.load();
+  if (gpu_failures) *gpu_failures = g_gpu_failures.load();
+}
 
 int kvsep_crc32c_batch_host_span(kvsep_crc32c_ctx* c, const char* host_base, uint64_t span_bytes,
                                  const uint64_t* off, const uint64_t* len, const uint32_t* init, uint32_t* out,

@@ -50,6 +50,7 @@ _SIGS = {
     "kvsep_crc32c_unmask": (ctypes.c_uint32, [ctypes.c_uint32]),
     "kvsep_accelerated_crc32c": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
     "kvsep_set_offload_threshold": (None, [ctypes.c_uint64]),
+    "kvsep_offload_stats": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "kvsep_crc32c_extend_host": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
     "kvsep_crc32c_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "kvsep_crc32c_ctx_destroy": (None, [ctypes.c_void_p]),

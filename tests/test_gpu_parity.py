@@ -236,16 +236,30 @@ def test_host_span_block_larger_than_staging(ctx, oracle):
     assert np.array_equal(ctx.batch_host_span(data, off, ln, np.array([7, 9], np.uint32)), exp)
 
 
+def offload_stats():
+    import ctypes
+    v = [ctypes.c_uint64(0) for _ in range(3)]
+    kvsep.lib().kvsep_offload_stats(*[ctypes.byref(x) for x in v])
+    return [x.value for x in v]
+
+
 def test_dropin_extend_offload_path(golden):
-    kvsep.lib().kvsep_set_offload_threshold(0)  # force every Extend through the GPU
+    kvsep.lib().kvsep_set_offload_threshold(1)  # force every non-empty Extend through the GPU
+    gpu0, host0, fail0 = offload_stats()
     try:
+        calls = 0
         for k in golden["known"]:
             dat = bytes.fromhex(k["hex"]) if k["hex"] is not None else bytes([k["fill"]["byte"]]) * k["fill"]["n"]
             assert kvsep.value(dat) == k["value"], k["name"]
+            calls += len(dat) > 0
         assert kvsep.lib().kvsep_accelerated_crc32c(0, b"TestCRCBuffer", 13) == 0xDCBC59FA
         assert kvsep.value(b"hello world") == kvsep.extend(kvsep.value(b"hello "), b"world")
+        calls += 4
     finally:
         kvsep.lib().kvsep_set_offload_threshold(64 << 20)
+    gpu1, host1, fail1 = offload_stats()
+    # every one of those calls ran on the GPU: none on the host leg, no silent host fallback
+    assert (gpu1 - gpu0, fail1 - fail0) == (calls, 0)
 
 
 def test_split_invariance_full_cfg3_scale(ctx):
