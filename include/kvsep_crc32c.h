@@ -120,6 +120,11 @@ uint64_t kvsep_log_walk(const char* buf, uint64_t n, uint64_t* off, uint64_t* le
                         uint64_t cap);
 int kvsep_log_verify_host(kvsep_crc32c_ctx* ctx, const char* buf, uint64_t n, uint8_t* ok, uint64_t cap,
                           uint64_t* nrecords);
+/* What log::Reader::ReadPhysicalRecord returns, given the walk (off as from kvsep_log_walk) and each record's
+ * checksum verdict ok[i]: a mismatch drops the rest of its 32 KiB block buffer (db/log_reader.cc:250-258), so
+ * that record and every later record of the same block get accept[i] = 0.  Returns the bytes reported as
+ * dropped with "checksum mismatch" (header of the bad record to the end of its block, or of the file). */
+uint64_t kvsep_log_accept(const uint64_t* off, const uint8_t* ok, uint64_t count, uint64_t n, uint8_t* accept);
 /* SST block trailers (table/table_builder.cc:209-232): masked_out[i] = Mask(Extend(Value(block_i), &types[i], 1)),
  * the LE32 word written after the type byte.  Device pointers, async on stream. */
 int kvsep_sst_trailers_device(kvsep_crc32c_ctx* ctx, void* stream, const void* base, const uint64_t* off,

@@ -143,4 +143,24 @@ int kvsep_log_verify_host(kvsep_crc32c_ctx* ctx, const char* buf, uint64_t n, ui
   return KVSEP_OK;
 }
 
+uint64_t kvsep_log_accept(const uint64_t* off, const uint8_t* ok, uint64_t count, uint64_t n, uint8_t* accept) {
+  uint64_t dropped = 0, dead_block = ~0ull;
+  for (uint64_t i = 0; i < count; ++i) {
+    const uint64_t hdr = off[i] - 6, blk = hdr / kLogBlock;
+    if (blk == dead_block) {  // already dropped with the buffer
+      accept[i] = 0;
+      continue;
+    }
+    if (ok[i]) {
+      accept[i] = 1;
+      continue;
+    }
+    accept[i] = 0;
+    const uint64_t end = (blk + 1) * kLogBlock < n ? (blk + 1) * kLogBlock : n;
+    dropped += end - hdr;  // drop_size = buffer_.size() (:255-257)
+    dead_block = blk;
+  }
+  return dropped;
+}
+
 }  // extern "C"

@@ -86,6 +86,8 @@ _SIGS = {
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
     "kvsep_log_verify_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                              ctypes.c_uint64, ctypes.c_void_p]),
+    "kvsep_log_accept": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                           ctypes.c_void_p]),
     "kvsep_sst_trailers_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                                  ctypes.c_uint64, ctypes.c_uint64]),
@@ -367,6 +369,17 @@ def log_walk(image):
     lib().kvsep_log_walk(p, keep.nbytes, off.ctypes.data_as(ctypes.c_void_p), ln.ctypes.data_as(ctypes.c_void_p),
                          st.ctypes.data_as(ctypes.c_void_p), ty.ctypes.data_as(ctypes.c_void_p), cnt)
     return off, ln, st, ty
+
+
+def log_accept(off, ok, n: int):
+    """log::Reader acceptance (db/log_reader.cc:250-258) from the walk and per-record checksum verdicts ->
+    (accept 0/1 array, bytes reported dropped with "checksum mismatch")."""
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    ok = np.ascontiguousarray(ok, dtype=np.uint8)
+    acc = np.zeros(max(off.size, 1), np.uint8)
+    dropped = lib().kvsep_log_accept(off.ctypes.data_as(ctypes.c_void_p), ok.ctypes.data_as(ctypes.c_void_p),
+                                     off.size, n, acc.ctypes.data_as(ctypes.c_void_p))
+    return acc[:off.size], int(dropped)
 
 
 def fill_splitmix64(dst, nbytes: int, seed: int, stream_offset: int = 0, stream=None):

@@ -48,6 +48,33 @@ def test_log_walk_matches_writer_fragments(oracle):
     assert {2, 3, 4} <= set(ty.tolist())  # FIRST / MIDDLE / LAST fragments present
 
 
+def test_log_accept_checksum_mismatch_like_log_test(oracle):
+    """db/log_test.cc:413-418 ChecksumMismatch: one 3-byte record with a bad checksum -> nothing returned and
+    10 bytes (7-byte header + payload) reported dropped."""
+    img, phys = log_image([b"foo"], oracle)
+    off = kvsep.log_walk(img)[0]
+    acc, dropped = kvsep.log_accept(off, [0], len(img))
+    assert acc.tolist() == [0] and dropped == 10
+    acc, dropped = kvsep.log_accept(off, [1], len(img))
+    assert acc.tolist() == [1] and dropped == 0
+
+
+def test_log_accept_drops_rest_of_block_only(oracle):
+    recs = _payloads(80, 5, 3000)
+    img, phys = log_image(recs, oracle)
+    off = kvsep.log_walk(img)[0]
+    blk = (off - 6) // 32768
+    ok = np.ones(off.size, np.uint8)
+    bad = int(np.flatnonzero(blk == 1)[2])   # third record of block 1
+    ok[bad] = 0
+    acc, dropped = kvsep.log_accept(off, ok, len(img))
+    expect = np.ones(off.size, np.uint8)
+    expect[bad:] = 0
+    expect[blk > 1] = 1                      # the reader resumes with the next block
+    assert np.array_equal(acc, expect)
+    assert dropped == 2 * 32768 - int(off[bad] - 6)
+
+
 def test_log_walk_stops_at_zero_padding_and_bad_length(oracle):
     img, phys = log_image([b"abc" * 10], oracle)
     padded = img + b"\x00" * 100                       # preallocated zeros (db/log_reader.cc:243-249)

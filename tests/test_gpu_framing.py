@@ -60,6 +60,13 @@ def test_log_manifest_verify(ctx, oracle):
     bad[h + 7] ^= 1                                      # payload byte of physical record 17
     ok = ctx.log_verify(bytes(bad))
     assert not ok[17] and ok.sum() == len(phys) - 1
+    # what log::Reader returns: record 17 and the rest of its 32 KiB block are dropped (db/log_reader.cc:250-258)
+    off = kvsep.log_walk(bytes(bad))[0]
+    acc, dropped = kvsep.log_accept(off, ok, len(bad))
+    blk = (off - 6) // 32768
+    same = blk == blk[17]
+    assert not acc[same & (np.arange(off.size) >= 17)].any() and acc[~same | (np.arange(off.size) < 17)].all()
+    assert dropped == min(int(blk[17] + 1) * 32768, len(bad)) - h
 
 
 def test_sst_trailers_and_verify(ctx, oracle):
