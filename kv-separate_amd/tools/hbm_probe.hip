@@ -160,7 +160,13 @@ int main(int argc, char** argv) {
   const size_t n16 = bytes / 16;
   u32x4* buf;
   unsigned* sink;
-  CHECK(hipMalloc(&buf, bytes));
+  if (argc > 2 && argv[2][0] == 'c') {  // physically contiguous allocation (hipDeviceMallocContiguous)
+    const hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&buf), bytes, hipDeviceMallocContiguous);
+    printf("contiguous allocation of %.1f GiB: %s\n", gib, hipGetErrorString(e));
+    if (e != hipSuccess) return 0;
+  } else {
+    CHECK(hipMalloc(&buf, bytes));
+  }
   CHECK(hipMalloc(&sink, 4));
   CHECK(hipMemset(buf, 0x5a, bytes));
   int cus = 0;
@@ -185,6 +191,15 @@ int main(int argc, char** argv) {
          size_t(CH) / 1024,                                                                             \
          timeit([&] { k_wavechunk_pol<U, POL><<<cus * WGPERCU, BLK>>>(buf, n16, size_t(CH) / 16, sink); }, \
                 reps, double(bytes)))
+  if (argc > 2 && (argv[2][0] == 'c' || argv[2][0] == 'p')) {  // allocation kind: contiguous ('c') vs plain ('p')
+    k_fill_random<<<cus * 8, 256>>>(buf, n16);
+    CHECK(hipDeviceSynchronize());
+    for (int i = 0; i < 2; ++i) {
+      WC(16, true, 512, 2, 1 << 20);
+      WG(8, true, 512, 1, 1 << 20);
+    }
+    return 0;
+  }
   if (argc > 2 && argv[2][0] == 'r') {  // constant vs random data, chunk size, at the best rows-in-flight
     WC(16, true, 512, 2, 1 << 20);
     WC(16, true, 512, 2, 128 << 10);
