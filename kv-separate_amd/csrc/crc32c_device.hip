@@ -1050,6 +1050,8 @@ int launch_batch(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* ba
                  const uint64_t* len, const uint32_t* init, const uint32_t* expect, uint32_t* out, uint64_t* first_bad,
                  uint64_t* nbad, uint64_t count, uint64_t total_bytes, uint64_t max_len) {
   if (!base || !off || !len || !out) return set_err(KVSEP_EINVAL, "null pointer argument");
+  // block indices travel as u32 through the descriptor windows and the piece table
+  if (count > 0xffffffffull) return set_err(KVSEP_EINVAL, "more than 2^32 - 1 blocks in one batch");
   KVSEP_HIP(hipSetDevice(c->device));
   int rc = acquire(sc, s);
   if (rc) return rc;
