@@ -152,6 +152,8 @@ def main():
     ap.add_argument("--piece-kib", type=int, default=0, help="work-item size (0 = library default)")
     ap.add_argument("--schedule", default="default", choices=["default", "static", "dynamic"])
     ap.add_argument("--no-plan-hint", action="store_true", help="pass max_len = 0 (force the planning pass)")
+    ap.add_argument("--launch", default="graph", choices=["graph", "eager"],
+                    help="timed steps as hipGraph replays (default; eager launches if capture fails) or eager")
     ap.add_argument("--cpu-sample-blocks", type=int, default=4096)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU work per thread count (>= 1 pass)")
@@ -212,22 +214,43 @@ def main():
     ctx.reserve(count, useful)
     stream = torch.cuda.current_stream()
 
-    def step():
+    def step(st):
         for _ in range(passes):
             ctx.batch_device(data.data_ptr(), d_off, d_len, out, count=count, total_bytes=useful, max_len=max_len,
-                             stream=stream)
+                             stream=st)
 
     for _ in range(args.warmup):
-        step()
+        step(stream)
     torch.cuda.synchronize()
+    # kernel-only time of the CRC kernel: HIP events on the launch stream, over eager steps
     ctx.get_timing()
     ctx.set_timing(True)
+    for _ in range(args.steps if args.launch == "graph" else 0):
+        step(stream)
+    torch.cuda.synchronize()
+
+    # the timed steps: one hipGraph replay per step (the step's planning kernels, memsets, CRC kernel(s) and
+    # combine captured once; kvsep_crc32c_reserve made every allocation beforehand), or eager launches
+    run = lambda: step(stream)  # noqa: E731
+    launch = "eager"
+    if args.launch == "graph":
+        ctx.set_timing(False)  # no timing events inside the graph
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                step(torch.cuda.current_stream())
+            g.replay()  # warm replay
+            torch.cuda.synchronize()
+            run, launch = g.replay, "hipGraph"
+        except Exception as e:  # keep the measurement: fall back to eager launches
+            log(f"[rank {rank}] graph capture failed ({e}); timing eager launches")
+            torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        run()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -316,6 +339,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
+            "launch": launch,
             "higher_is_better": True,
             "scaling": "strong" if args.config == "5" else "weak",
             "vs_baseline": None,

@@ -120,6 +120,13 @@ uint64_t kvsep_log_walk(const char* buf, uint64_t n, uint64_t* off, uint64_t* le
                         uint64_t cap);
 int kvsep_log_verify_host(kvsep_crc32c_ctx* ctx, const char* buf, uint64_t n, uint8_t* ok, uint64_t cap,
                           uint64_t* nrecords);
+/* log / MANIFEST write side (db/log_writer.cc:35-115): appends `count` records to a log of current length
+ * dest_length (the writer's block_offset_ = dest_length % 32 KiB, log_writer.cc:27-28), fragmenting each record
+ * over 32 KiB blocks as FULL / FIRST / MIDDLE / LAST physical records and zero-filling block trailers of
+ * fewer than 7 bytes; every fragment's crc = Mask(Extend(Value(&type, 1), fragment)) comes from ONE batched
+ * call.  dst receives the appended bytes; *written = their count (also on KVSEP_EINVAL for a short dst). */
+int kvsep_log_frame_host(kvsep_crc32c_ctx* ctx, const char* const* payload, const uint64_t* len, uint64_t count,
+                         uint64_t dest_length, char* dst, uint64_t dst_cap, uint64_t* written);
 /* What log::Reader::ReadPhysicalRecord returns, given the walk (off as from kvsep_log_walk) and each record's
  * checksum verdict ok[i]: a mismatch drops the rest of its 32 KiB block buffer (db/log_reader.cc:250-258), so
  * that record and every later record of the same block get accept[i] = 0.  Returns the bytes reported as

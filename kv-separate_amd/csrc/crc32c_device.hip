@@ -1053,11 +1053,18 @@ int launch_batch(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* ba
   // block indices travel as u32 through the descriptor windows and the piece table
   if (count > 0xffffffffull) return set_err(KVSEP_EINVAL, "more than 2^32 - 1 blocks in one batch");
   KVSEP_HIP(hipSetDevice(c->device));
-  int rc = acquire(sc, s);
+  // Under stream capture (hipGraph) the call only records its nodes: the cross-stream scratch events are
+  // skipped (a captured wait on an event recorded outside the capture is not allowed), so the graph's user
+  // orders its replays against other uses of this context's scratch.  Allocation must not happen either:
+  // kvsep_crc32c_reserve first.
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  KVSEP_HIP(hipStreamIsCapturing(s, &cap));
+  const bool capturing = cap != hipStreamCaptureStatusNone;
+  int rc = capturing ? KVSEP_OK : acquire(sc, s);
   if (rc) return rc;
   rc = launch_batch_in(c, sc, s, base, off, len, init, expect, out, first_bad, nbad, count, total_bytes, max_len);
   if (rc) return rc;
-  return release(sc, s);
+  return capturing ? KVSEP_OK : release(sc, s);
 }
 
 int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* base, const uint64_t* off,
@@ -1233,6 +1240,10 @@ int kvsep_crc32c_reserve(kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_byt
   if (!c) return set_err(KVSEP_EINVAL, "null ctx");
   std::lock_guard<std::mutex> g(c->mu);
   KVSEP_HIP(hipSetDevice(c->device));
+  // everything a later call could allocate, so that the call can be captured into a hipGraph
+  if (!c->sc.d_counter) KVSEP_HIP(hipMalloc(&c->sc.d_counter, 16));
+  if (!c->sc.d_verify) KVSEP_HIP(hipMalloc(&c->sc.d_verify, 16));
+  if (!c->sc.last_use) KVSEP_HIP(hipEventCreateWithFlags(&c->sc.last_use, hipEventDisableTiming));
   return ensure_plan(c->sc, c->piece_bytes, count, total_bytes);
 }
 

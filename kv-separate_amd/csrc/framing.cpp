@@ -143,6 +143,70 @@ int kvsep_log_verify_host(kvsep_crc32c_ctx* ctx, const char* buf, uint64_t n, ui
   return KVSEP_OK;
 }
 
+int kvsep_log_frame_host(kvsep_crc32c_ctx* ctx, const char* const* payload, const uint64_t* len, uint64_t count,
+                         uint64_t dest_length, char* dst, uint64_t dst_cap, uint64_t* written) {
+  if (!ctx || (count && (!payload || !len))) return KVSEP_EINVAL;
+  struct Frag {
+    const char* src;
+    uint64_t len, at;  // payload bytes; offset of its header in dst
+    uint8_t type;
+  };
+  std::vector<Frag> frags;
+  uint64_t block_offset = dest_length % kLogBlock, p = 0;
+  for (uint64_t r = 0; r < count; ++r) {  // log::Writer::AddRecord (:35-82)
+    const char* ptr = payload[r];
+    uint64_t left = len[r];
+    bool begin = true;
+    do {
+      const uint64_t leftover = kLogBlock - block_offset;
+      if (leftover < kLogHeader) {  // trailer: zero-filled, next block (:48-57)
+        p += leftover;
+        block_offset = 0;
+      }
+      const uint64_t avail = kLogBlock - block_offset - kLogHeader;
+      const uint64_t frag = left < avail ? left : avail;
+      const bool end = left == frag;
+      const uint8_t type = begin && end ? 1 : begin ? 2 : end ? 4 : 3;  // FULL / FIRST / LAST / MIDDLE
+      frags.push_back({ptr, frag, p, type});
+      p += kLogHeader + frag;
+      block_offset += kLogHeader + frag;
+      ptr += frag;
+      left -= frag;
+      begin = false;
+    } while (left > 0);
+  }
+  if (written) *written = p;
+  if (p > dst_cap || (p && !dst)) return KVSEP_EINVAL;
+  const uint64_t nf = frags.size();
+  std::vector<const char*> src(nf);
+  std::vector<uint64_t> flen(nf);
+  std::vector<uint32_t> init(nf), crc(nf);
+  uint32_t type_crc[5];
+  for (int t = 0; t < 5; ++t) {  // InitTypeCrc (:16-21)
+    const char c = char(t);
+    type_crc[t] = kvsep_crc32c_extend_host(0, &c, 1);
+  }
+  for (uint64_t i = 0; i < nf; ++i) {
+    src[i] = frags[i].src;
+    flen[i] = frags[i].len;
+    init[i] = type_crc[frags[i].type];
+  }
+  if (nf) {
+    const int rc = kvsep_crc32c_batch_host(ctx, init.data(), src.data(), flen.data(), crc.data(), nf);
+    if (rc) return rc;
+  }
+  if (p) std::memset(dst, 0, p);  // trailers
+  for (uint64_t i = 0; i < nf; ++i) {  // EmitPhysicalRecord (:84-115)
+    char* h = dst + frags[i].at;
+    put_le32(h, kvsep_crc32c_mask(crc[i]));
+    h[4] = char(frags[i].len & 0xff);
+    h[5] = char(frags[i].len >> 8);
+    h[6] = char(frags[i].type);
+    if (frags[i].len) std::memcpy(h + kLogHeader, frags[i].src, frags[i].len);
+  }
+  return KVSEP_OK;
+}
+
 uint64_t kvsep_log_accept(const uint64_t* off, const uint8_t* ok, uint64_t count, uint64_t n, uint8_t* accept) {
   uint64_t dropped = 0, dead_block = ~0ull;
   for (uint64_t i = 0; i < count; ++i) {

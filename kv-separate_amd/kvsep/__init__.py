@@ -86,6 +86,8 @@ _SIGS = {
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
     "kvsep_log_verify_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                              ctypes.c_uint64, ctypes.c_void_p]),
+    "kvsep_log_frame_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                            ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     "kvsep_log_accept": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                            ctypes.c_void_p]),
     "kvsep_sst_trailers_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -314,6 +316,21 @@ class Context:
         _check(lib().kvsep_vlog_frame_host(self._h, ptrs, lens.ctypes.data_as(ctypes.c_void_p), k,
                                            dst.ctypes.data_as(ctypes.c_void_p), dst.nbytes, ctypes.byref(w)),
                "kvsep_vlog_frame_host")
+        return dst[:w.value].tobytes()
+
+    def log_frame(self, records, dest_length: int = 0):
+        """db/log_writer.cc:35-115: AddRecord of each record onto a log of length dest_length -> appended bytes."""
+        keep = [_buf(b) for b in records]
+        k = len(records)
+        ptrs = (ctypes.c_void_p * max(k, 1))(*[x[0].value for x in keep])
+        lens = np.array([x[1].nbytes for x in keep], dtype=np.uint64)
+        w = ctypes.c_uint64()
+        lib().kvsep_log_frame_host(self._h, ptrs, lens.ctypes.data_as(ctypes.c_void_p), k, dest_length, None, 0,
+                                   ctypes.byref(w))  # sizing call: *written even when dst is short
+        dst = np.zeros(max(w.value, 1), dtype=np.uint8)
+        _check(lib().kvsep_log_frame_host(self._h, ptrs, lens.ctypes.data_as(ctypes.c_void_p), k, dest_length,
+                                          dst.ctypes.data_as(ctypes.c_void_p), dst.nbytes, ctypes.byref(w)),
+               "kvsep_log_frame_host")
         return dst[:w.value].tobytes()
 
     def log_verify(self, image):

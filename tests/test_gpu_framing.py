@@ -69,6 +69,17 @@ def test_log_manifest_verify(ctx, oracle):
     assert dropped == min(int(blk[17] + 1) * 32768, len(bad)) - h
 
 
+def test_log_manifest_write_side(ctx, oracle):
+    """log::Writer::AddRecord batched: identical bytes to an independently framed image, also when appending to
+    a log that already ends mid-block (block_offset_ = dest_length % 32 KiB) and with trailers < 7 bytes."""
+    recs = _payloads(70, 15, 90000) + [b"", b"x" * 32761, b"y" * 32755, b"z" * 40000]
+    img, _ = log_image(recs, oracle)
+    assert ctx.log_frame(recs) == img
+    head, _ = log_image(recs[:23], oracle)
+    assert head + ctx.log_frame(recs[23:], dest_length=len(head)) == img
+    assert (ctx.log_verify(img) == 1).all()
+
+
 def test_sst_trailers_and_verify(ctx, oracle):
     blocks = _payloads(2000, 14, 8192, minlen=1)
     types = np.random.default_rng(1).integers(0, 2, len(blocks)).astype(np.uint8)  # kNoCompression / kSnappy
