@@ -262,6 +262,30 @@ def test_dropin_extend_offload_path(golden):
     assert (gpu1 - gpu0, fail1 - fail0) == (calls, 0)
 
 
+def test_dropin_extend_concurrent_threads(oracle):
+    """Extend is called concurrently by the writer, compaction and GC threads: 8 threads
+    through the GPU leg at once, each result bit-exact, none served by the host fallback."""
+    import threading
+    bufs = [splitmix64_bytes(300_000 + 4099 * i, 70 + i, 0).tobytes() for i in range(8)]
+    exp = [oracle.extend(0, b) for b in bufs]
+    got = [None] * 8
+    kvsep.lib().kvsep_set_offload_threshold(1)
+    gpu0, _, fail0 = offload_stats()
+    try:
+        def work(i):
+            got[i] = [kvsep.value(bufs[i]) for _ in range(5)]
+        ts = [threading.Thread(target=work, args=(i,)) for i in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    finally:
+        kvsep.lib().kvsep_set_offload_threshold(64 << 20)
+    gpu1, _, fail1 = offload_stats()
+    assert got == [[e] * 5 for e in exp]
+    assert (gpu1 - gpu0, fail1 - fail0) == (40, 0)
+
+
 def test_split_invariance_full_cfg3_scale(ctx):
     """Size-independent property on 2048 x 1 MiB: CRC(block) == Extend(CRC(first k bytes), rest)."""
     off, ln = W.cfg3_layout(count=2048)
