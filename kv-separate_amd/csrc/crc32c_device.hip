@@ -1126,9 +1126,16 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     if (e0 && e1) KVSEP_HIP(hipEventRecord(e0, s));
   }
   if (!planned && c->narrow && max_len <= kNarrowMax) {
-    switch (c->narrow) {  // 1: 16-wave workgroups (default); 2: 8 waves; 3: 12 waves
+    // 1 (default): 16-wave workgroups below 128 Ki blocks, 8-wave ones from there on.  A small batch gives each
+    // wave only a couple of 8-block groups, and more waves hide more of the launch/first-load ramp (256 MiB
+    // of 4 KiB blocks: 16 waves +5 %); a large one streams better with 8 (4 GiB of 4 KiB blocks: +3 %).
+    // 2: always 8 waves; 3: 12 waves; 4 / 5: 8-row groups at 8 / 12 waves; 6: always 16 waves.
+    const int nv = c->narrow == 1 ? (count >= (1u << 17) ? 2 : 6) : c->narrow;
+    switch (nv) {
       case 2: crc32c_narrow_kernel<4, true, 512><<<grid, 512, 0, s>>>(a); break;
       case 3: crc32c_narrow_kernel<4, true, 768><<<grid, 768, 0, s>>>(a); break;
+      case 4: crc32c_narrow_kernel<8, true, 512><<<grid, 512, 0, s>>>(a); break;
+      case 5: crc32c_narrow_kernel<8, true, 768><<<grid, 768, 0, s>>>(a); break;
       default: crc32c_narrow_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
     }
   } else {
