@@ -261,6 +261,7 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * passes * useful * args.steps / GIB / elapsed
     kern_avg_ms = kern_ms / max(1, launches)
+    kernel_name = ctx.kernel_name(count, max_len)
     achieved_gbps = useful / (kern_avg_ms * 1e-3) / 1e9
 
     # ---- outside the timed region: result digest gather (RCCL), parity spot check, ceilings
@@ -350,8 +351,7 @@ def main():
                        "parallelism": f"shard{world} (independent blocks per GPU, no data-path collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved_gbps / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel": ("crc32c_narrow_kernel" if 0 < max_len <= kvsep.NARROW_MAX_LEN
-                                    else "crc32c_pieces_kernel"), "kernel_avg_ms": round(kern_avg_ms, 4),
+                         "kernel": kernel_name, "kernel_avg_ms": round(kern_avg_ms, 4),
                          "algorithmic_bytes_per_launch": useful},
             "cpu_baseline": cpu,
             "read_ceiling_GBps": read_ceiling_gbps and round(read_ceiling_gbps, 1),

@@ -69,6 +69,9 @@ int kvsep_crc32c_reserve(kvsep_crc32c_ctx* ctx, uint64_t count, uint64_t total_b
 /* Kernel timing with HIP events on the caller's stream, around the main CRC kernel only. */
 int kvsep_crc32c_ctx_set_timing(kvsep_crc32c_ctx* ctx, int enable);
 int kvsep_crc32c_ctx_get_timing(kvsep_crc32c_ctx* ctx, double* total_ms, uint64_t* launches); /* syncs + resets */
+/* Name of the main kernel a batch of `count` blocks with this max_len hint runs on ("crc32c_pieces_kernel" or
+ * "crc32c_narrow_kernel"): the kernel the timing above and a rocprofv3 trace refer to. */
+const char* kvsep_crc32c_kernel_name(kvsep_crc32c_ctx* ctx, uint64_t count, uint64_t max_len);
 
 /* ---------------------------------------------------------------- batched device form
  * out[i] = Extend(init ? init[i] : 0, base + off[i], len[i]) for i < count.

@@ -586,7 +586,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
 // 128-B lines, one per slot.
 constexpr int kNarrowLanes = 8;
 constexpr uint32_t kNarrowRow = 16u * kNarrowLanes;
-constexpr uint64_t kNarrowMax = 64 * 1024;  // host routes a batch here when its max_len hint is <= this
+constexpr uint64_t kNarrowMax = 32 * 1024;  // longest block the narrow kernel is ever chosen for (use_narrow)
 
 template <int kG>
 struct NStaged {
@@ -903,7 +903,7 @@ struct kvsep_crc32c_ctx {
   int dynamic = -1;  // -1 auto, 0 static, 1 guided
   int variant = 1;   // rows per prefetch group / load policy, see launch_pieces
   uint32_t static_contig = 1;
-  int narrow = 1;    // route batches of short blocks (max_len hint <= kNarrowMax) to the narrow kernel
+  int narrow = 1;    // route batches of short blocks to the narrow kernel (use_narrow; 0 = never)
   Scratch sc;  // scratch of the calls made directly on this context (any stream, event-ordered)
   // timing
   bool timing = false;
@@ -994,6 +994,21 @@ int ensure_plan(Scratch& sc, uint64_t piece_bytes, uint64_t count, uint64_t tota
   sc.cap_count = nc;
   sc.cap_pieces = np;
   return KVSEP_OK;
+}
+
+// Narrow or wide kernel for an unsplit batch (every block <= piece_bytes, known from the max_len hint)?  The
+// narrow kernel's unit of parallelism is an 8-block group, so it needs many blocks; it wins on short blocks
+// when there are enough of them (measured, tools/ab_variants.py on one MI355X):
+//   <= 8 KiB blocks from 16 Ki blocks up (1 M x 4 KiB: 6.67 vs 3.7 TB/s; 4 Ki x 4 KiB: the wide kernel wins),
+//   <= 32 KiB blocks from 32 Ki blocks up (32 Ki x 16 KiB: 6.05 vs 5.94; 16 Ki x 32 KiB: wide 6.25 vs 5.25),
+//   64 KiB blocks never (16 Ki x 64 KiB: wide 6.22 vs 4.88).
+// The thresholds scale with the CU count (256 on MI355X).
+// KVSEP_NARROW: 0 never, 1 this rule (default), 2..7 always when max_len <= 64 KiB (tests, A/B).
+bool use_narrow(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t max_len) {
+  if (!c->narrow || max_len == 0) return false;
+  if (c->narrow >= 2) return max_len <= 2 * kNarrowMax;
+  const uint64_t cus = uint64_t(c->num_cus);
+  return (max_len <= 8 * 1024 && count >= 64 * cus) || (max_len <= kNarrowMax && count >= 128 * cus);
 }
 
 hipEvent_t take_event(kvsep_crc32c_ctx* c) {
@@ -1125,12 +1140,12 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     e1 = take_event(c);
     if (e0 && e1) KVSEP_HIP(hipEventRecord(e0, s));
   }
-  if (!planned && c->narrow && max_len <= kNarrowMax) {
+  if (!planned && use_narrow(c, count, max_len)) {
     // 1 (default): 16-wave workgroups below 128 Ki blocks, 8-wave ones from there on.  A small batch gives each
     // wave only a couple of 8-block groups, and more waves hide more of the launch/first-load ramp (256 MiB
     // of 4 KiB blocks: 16 waves +5 %); a large one streams better with 8 (4 GiB of 4 KiB blocks: +3 %).
-    // 2: always 8 waves; 3: 12 waves; 4 / 5: 8-row groups at 8 / 12 waves; 6: always 16 waves.
-    const int nv = c->narrow == 1 ? (count >= (1u << 17) ? 2 : 6) : c->narrow;
+    // 2: always 8 waves; 3: 12 waves; 4 / 5: 8-row groups at 8 / 12 waves; 6: always 16 waves; 7: as 1.
+    const int nv = (c->narrow == 1 || c->narrow == 7) ? (count >= (1u << 17) ? 2 : 6) : c->narrow;
     switch (nv) {
       case 2: crc32c_narrow_kernel<4, true, 512><<<grid, 512, 0, s>>>(a); break;
       case 3: crc32c_narrow_kernel<4, true, 768><<<grid, 768, 0, s>>>(a); break;
@@ -1364,6 +1379,12 @@ int kvsep_sst_verify_device(kvsep_crc32c_ctx* c, void* stream, const void* file_
                        total_bytes + count, max_len ? max_len + 1 : 0);
   if (rc) return rc;
   return release(sc, s);
+}
+
+const char* kvsep_crc32c_kernel_name(kvsep_crc32c_ctx* c, uint64_t count, uint64_t max_len) {
+  if (!c) return "";
+  const bool planned = !(max_len != 0 && max_len <= c->piece_bytes);
+  return !planned && use_narrow(c, count, max_len) ? "crc32c_narrow_kernel" : "crc32c_pieces_kernel";
 }
 
 int kvsep_stream_read_device(kvsep_crc32c_ctx* c, void* stream, const void* src, uint64_t nbytes, uint32_t* sink) {

@@ -51,6 +51,7 @@ _SIGS = {
     "kvsep_accelerated_crc32c": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
     "kvsep_set_offload_threshold": (None, [ctypes.c_uint64]),
     "kvsep_offload_stats": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "kvsep_crc32c_kernel_name": (ctypes.c_char_p, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]),
     "kvsep_crc32c_extend_host": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
     "kvsep_crc32c_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "kvsep_crc32c_ctx_destroy": (None, [ctypes.c_void_p]),
@@ -191,7 +192,6 @@ def _dptr(t):
 
 
 DEFAULT_PIECE_BYTES = 128 * 1024  # the library default (kvsep_crc32c_ctx, crc32c_device.hip)
-NARROW_MAX_LEN = 64 * 1024  # batches whose max_len hint is <= this run the narrow kernel (kNarrowMax)
 
 
 class Context:
@@ -228,6 +228,10 @@ class Context:
 
     def reserve(self, count: int, total_bytes: int):
         _check(lib().kvsep_crc32c_reserve(self._h, count, total_bytes), "reserve")
+
+    def kernel_name(self, count: int, max_len: int) -> str:
+        """The main kernel a batch of `count` blocks with this max_len hint runs on."""
+        return lib().kvsep_crc32c_kernel_name(self._h, count, max_len).decode()
 
     def set_timing(self, on: bool):
         _check(lib().kvsep_crc32c_ctx_set_timing(self._h, 1 if on else 0), "set_timing")

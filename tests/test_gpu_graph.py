@@ -29,7 +29,7 @@ def test_capture_and_replay(layout, oracle):
     if layout == "planned":
         off, ln = W.cfg3_layout(vlog=True, count=96)  # 1,048,609-B records at odd offsets: 9 pieces each
     else:
-        off, ln = W.uniform_layout(5000, 4096, 4099, 3)  # 4 KiB blocks at odd offsets
+        off, ln = W.uniform_layout(20000, 4096, 4099, 3)  # 4 KiB blocks at odd offsets (narrow kernel)
     span = int(off[-1] + ln[-1])
     data = torch.empty(span + 64, dtype=torch.uint8, device=DEV)
     d_off, d_len = u64(off), u64(ln)
@@ -37,6 +37,8 @@ def test_capture_and_replay(layout, oracle):
     ctx = kvsep.Context(0)
     try:
         ctx.reserve(off.size, int(ln.sum()))
+        assert ctx.kernel_name(off.size, int(ln.max())) == (
+            "crc32c_pieces_kernel" if layout == "planned" else "crc32c_narrow_kernel")
         kvsep.fill_splitmix64(data.data_ptr(), span, 1, 0)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
