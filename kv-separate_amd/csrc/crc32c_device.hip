@@ -56,8 +56,10 @@ struct DevTables {
   uint32_t byte1[256];      // kByteOff
   uint32_t zpiece[4][256];  // Z_piece_bytes, used by the combine kernel
   uint32_t znarrow[4][256]; // Z_{16 kNarrowLanes}: the replicated table of the narrow kernel
+  uint32_t zsmall[3][4][256];  // Z_16K, Z_32K, Z_64K: the automatic smaller pieces of small batches
 };
-static_assert(sizeof(DevTables) == 4096 * 10 + 1024, "table layout");
+static_assert(sizeof(DevTables) == 4096 * 13 + 1024, "table layout");
+constexpr uint64_t kSmallPiece = 16 * 1024;  // zsmall[k] is Z_{kSmallPiece << k}
 
 struct PiecesArgs {
   const uint8_t* base;
@@ -73,7 +75,8 @@ struct PiecesArgs {
   const uint32_t* pblk;             // planned mode: block of piece g
   uint32_t* partial;                // planned mode: raw register of piece g
   uint32_t* work_counter;           // dynamic schedule
-  uint64_t piece_bytes;
+  uint64_t piece_bytes;             // of this batch (see piece_for)
+  const uint32_t* zpiece;           // Z_piece_bytes as 4 byte tables (combine kernel)
   uint64_t max_pieces;              // capacity of pblk/partial
   uint32_t static_contig;           // static schedule: contiguous item ranges per wave (else round-robin)
   const DevTables* tabs;
@@ -784,7 +787,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
 // One thread per block: Horner over the block's pieces, R <- Z_piece(R) ^ R_piece.
 __global__ void __launch_bounds__(256) crc32c_combine_kernel(PiecesArgs a) {
   __shared__ uint32_t zp[1024];
-  for (uint32_t i = threadIdx.x; i < 1024; i += 256) zp[i] = (&a.tabs->zpiece[0][0])[i];
+  for (uint32_t i = threadIdx.x; i < 1024; i += 256) zp[i] = a.zpiece[i];
   __syncthreads();
   const uint64_t b = uint64_t(blockIdx.x) * 256 + threadIdx.x;
   if (b >= a.count) return;
@@ -900,6 +903,7 @@ struct kvsep_crc32c_ctx {
   int num_cus = 0;
   DevTables* d_tabs = nullptr;
   uint64_t piece_bytes = 128 * 1024;  // best of 32 KiB .. 1 MiB on configs 3a/3b/4
+  bool piece_auto = true;             // smaller pieces for small batches (piece_for); off once set explicitly
   int dynamic = -1;  // -1 auto, 0 static, 1 guided
   int variant = 1;   // rows per prefetch group / load policy, see launch_pieces
   uint32_t static_contig = 1;
@@ -940,6 +944,7 @@ int upload_tables(kvsep_crc32c_ctx* c) {
   for (int j = 0; j < 6; ++j) gf2::byte_tables(gf2::zero_bytes_map(16ull << j), &h.ztree[j][0][0]);
   for (uint32_t b = 0; b < 256; ++b) h.byte1[b] = gf2::byte_table_entry(b);
   gf2::byte_tables(gf2::zero_bytes_map(c->piece_bytes), &h.zpiece[0][0]);
+  for (int k = 0; k < 3; ++k) gf2::byte_tables(gf2::zero_bytes_map(kSmallPiece << k), &h.zsmall[k][0][0]);
   gf2::byte_tables(gf2::zero_bytes_map(kNarrowRow), &h.znarrow[0][0]);
   if (!c->d_tabs) KVSEP_HIP(hipMalloc(&c->d_tabs, sizeof(DevTables)));
   KVSEP_HIP(hipMemcpy(c->d_tabs, &h, sizeof(DevTables), hipMemcpyHostToDevice));
@@ -1009,6 +1014,21 @@ bool use_narrow(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t max_len) {
   if (c->narrow >= 2) return max_len <= 2 * kNarrowMax;
   const uint64_t cus = uint64_t(c->num_cus);
   return (max_len <= 8 * 1024 && count >= 64 * cus) || (max_len <= kNarrowMax && count >= 128 * cus);
+}
+
+// Piece size of a planned batch.  With the default setting, a batch too small to give every wave two pieces
+// of piece_bytes gets 64, 32 or 16 KiB pieces instead: the largest size that still makes >= 2 pieces per wave
+// (64 blocks of 1 MiB: 16 KiB pieces).  Large batches keep piece_bytes.
+uint64_t piece_for(const kvsep_crc32c_ctx* c, uint64_t total_bytes, const uint32_t** zp) {
+  *zp = &c->d_tabs->zpiece[0][0];
+  if (!c->piece_auto) return c->piece_bytes;
+  const uint64_t want = 2 * uint64_t(c->num_cus) * (kWgThreads / 64);
+  uint64_t P = c->piece_bytes;
+  for (int k = 2; k >= 0 && total_bytes / P < want; --k) {
+    P = kSmallPiece << k;
+    *zp = &c->d_tabs->zsmall[k][0][0];
+  }
+  return P;
 }
 
 hipEvent_t take_event(kvsep_crc32c_ctx* c) {
@@ -1094,7 +1114,7 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
   a.out = out;
   a.expect = expect;
   a.count = count;
-  a.piece_bytes = c->piece_bytes;
+  a.piece_bytes = planned ? piece_for(c, total_bytes, &a.zpiece) : c->piece_bytes;
   a.tabs = c->d_tabs;
   if (expect) {
     if (!first_bad || !nbad) {
@@ -1109,14 +1129,14 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
   }
   if (count == 0) return KVSEP_OK;
   if (planned) {
-    int rc = ensure_plan(sc, c->piece_bytes, count, total_bytes);
+    int rc = ensure_plan(sc, a.piece_bytes, count, total_bytes);
     if (rc) return rc;
     a.pstart = sc.d_pstart;
     a.pblk = sc.d_pblk;
     a.partial = sc.d_partial;
     a.max_pieces = sc.cap_pieces;
     const unsigned nb = unsigned((count + 255) / 256);
-    crc32c_plan_count_kernel<<<nb, 256, 0, s>>>(len, count, c->piece_bytes, sc.d_counts);
+    crc32c_plan_count_kernel<<<nb, 256, 0, s>>>(len, count, a.piece_bytes, sc.d_counts);
     KVSEP_HIP(hipGetLastError());
     KVSEP_HIP(hipMemsetAsync(sc.d_pstart, 0, 4, s));
     size_t tb = sc.scan_tmp_bytes;
@@ -1126,7 +1146,12 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
   } else {
     a.max_pieces = count;
   }
-  const bool dyn = c->dynamic < 0 ? planned : c->dynamic == 1;  // auto: guided when planned, else static
+  // auto schedule: guided (one atomic per grab) for planned batches with many pieces; static for the rest --
+  // a few thousand small pieces would spend most of the kernel in single-item grabs on one counter
+  // (~88 dequeues/us, MI355X_MICROARCH.md dequeue)
+  const uint64_t est_items = planned ? count + total_bytes / a.piece_bytes : count;
+  const uint64_t nwaves_est = uint64_t(c->num_cus) * (kWgThreads / 64);
+  const bool dyn = c->dynamic < 0 ? (planned && est_items >= 8 * nwaves_est) : c->dynamic == 1;
   a.static_contig = c->static_contig;
   if (dyn) {
     if (!sc.d_counter) KVSEP_HIP(hipMalloc(&sc.d_counter, 16));
@@ -1247,6 +1272,7 @@ int kvsep_crc32c_ctx_set_piece_bytes(kvsep_crc32c_ctx* c, uint64_t piece_bytes) 
   KVSEP_HIP(hipSetDevice(c->device));
   KVSEP_HIP(hipDeviceSynchronize());
   c->piece_bytes = piece_bytes;
+  c->piece_auto = false;
   free_plan(c->sc);  // piece tables depend on piece_bytes (device already idle)
   for (auto& sc : c->staging.scratch) free_plan(sc);
   return upload_tables(c);
@@ -1266,7 +1292,8 @@ int kvsep_crc32c_reserve(kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_byt
   if (!c->sc.d_counter) KVSEP_HIP(hipMalloc(&c->sc.d_counter, 16));
   if (!c->sc.d_verify) KVSEP_HIP(hipMalloc(&c->sc.d_verify, 16));
   if (!c->sc.last_use) KVSEP_HIP(hipEventCreateWithFlags(&c->sc.last_use, hipEventDisableTiming));
-  return ensure_plan(c->sc, c->piece_bytes, count, total_bytes);
+  const uint32_t* zp = nullptr;
+  return ensure_plan(c->sc, piece_for(c, total_bytes, &zp), count, total_bytes);
 }
 
 int kvsep_crc32c_ctx_set_timing(kvsep_crc32c_ctx* c, int enable) {
