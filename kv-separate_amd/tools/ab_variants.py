@@ -5,7 +5,7 @@ usage: python ab_variants.py --variants 1,2 --configs 3a,2 --rounds 5 --steps 5
 Prints per (config, variant) the median / min kernel time and GB/s (kernel-only HIP events).
 A variant written "b<N>" runs variant N of a second build of the library (--lib-b), so two source versions
 are compared in one process on one box; "n<K>" selects narrow-kernel variant K (KVSEP_NARROW) for short blocks;
-"<N>p<KiB>" runs variant N with its own piece size.
+"<N>p<KiB>" runs variant N with its own piece size; a trailing "s" / "d" forces the static / guided schedule.
 """
 import argparse
 import os
@@ -53,6 +53,9 @@ def main():
         use(v)
         code = v[1:] if v.startswith("b") else v
         piece_kib = args.piece_kib
+        sched = None
+        if code.endswith("s") or code.endswith("d"):  # "<variant>s" / "<variant>d": static / guided schedule
+            sched, code = code[-1] == "d", code[:-1]
         if "p" in code:  # "<variant>p<KiB>": that variant with its own piece size, e.g. 1p128 vs 1p1024
             code, pk = code.split("p")
             piece_kib = int(pk)
@@ -63,6 +66,8 @@ def main():
         ctxs[v] = kvsep.Context(0)
         if piece_kib:
             ctxs[v].set_piece_bytes(piece_kib * 1024)
+        if sched is not None:
+            ctxs[v].set_schedule(sched)
     dev = torch.device("cuda:0")
     for cfg in args.configs.split(","):
         off, ln = layout(cfg)
