@@ -10,6 +10,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <thread>
+#include <vector>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -22,6 +25,81 @@
 
 namespace kvsep {
 
+// ------------------------------------------------------------------ parallel staging copies
+class CopyPool {
+ public:
+  explicit CopyPool(int nthreads) {
+    for (int i = 0; i < nthreads; ++i) th_.emplace_back([this] { worker(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  // Chunks of <= 1 MiB are claimed from one counter by the workers and the caller alike.
+  void run(const CopySeg* segs, uint64_t nseg) {
+    chunks_.clear();
+    for (uint64_t i = 0; i < nseg; ++i)
+      for (uint64_t o = 0; o < segs[i].n; o += kChunk)
+        chunks_.push_back({segs[i].dst + o, segs[i].src + o, std::min<uint64_t>(kChunk, segs[i].n - o)});
+    if (chunks_.size() <= 2 || th_.empty()) {  // not worth waking anyone
+      for (auto& c : chunks_) std::memcpy(c.dst, c.src, c.n);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(m_);
+      next_.store(0);
+      active_ = int(th_.size());
+      ++gen_;
+    }
+    cv_.notify_all();
+    drain();
+    std::unique_lock<std::mutex> lk(m_);
+    done_cv_.wait(lk, [this] { return active_ == 0; });
+  }
+
+ private:
+  static constexpr uint64_t kChunk = 1ull << 20;
+  void drain() {
+    for (uint64_t k; (k = next_.fetch_add(1)) < chunks_.size();) std::memcpy(chunks_[k].dst, chunks_[k].src, chunks_[k].n);
+  }
+  void worker() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      drain();
+      std::lock_guard<std::mutex> g(m_);
+      if (--active_ == 0) done_cv_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::vector<CopySeg> chunks_;
+  std::atomic<uint64_t> next_{0};
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  uint64_t gen_ = 0;
+  int active_ = 0;
+  bool stop_ = false;
+};
+
+CopyPool* copy_pool_create() {
+  int n = 7;  // + the caller: 8 copiers
+  if (const char* v = std::getenv("KVSEP_COPY_THREADS")) n = std::max(0, std::atoi(v) - 1);
+  const int hw = int(std::thread::hardware_concurrency());
+  if (hw > 0) n = std::min(n, std::max(0, hw - 1));
+  return new CopyPool(n);
+}
+void copy_pool_destroy(CopyPool* p) { delete p; }
+void copy_pool_run(CopyPool* p, const CopySeg* segs, uint64_t nseg) { p->run(segs, nseg); }
+
 void release_staging(HostStaging& s) {
   for (int i = 0; i < HostStaging::kSlots; ++i) {
     if (s.stream[i]) hipStreamSynchronize(s.stream[i]);
@@ -31,6 +109,7 @@ void release_staging(HostStaging& s) {
     free_scratch(s.scratch[i]);
     if (s.stream[i]) hipStreamDestroy(s.stream[i]);
   }
+  copy_pool_destroy(s.pool);
   s = HostStaging();
 }
 
@@ -152,6 +231,7 @@ int ensure_staging(kvsep_crc32c_ctx* c) {
     KVSEP_HIPH(hipStreamCreateWithFlags(&s.stream[i], hipStreamNonBlocking));
     KVSEP_HIPH(hipEventCreateWithFlags(&s.done[i], hipEventDisableTiming));
   }
+  s.pool = copy_pool_create();
   s.ready = true;
   return KVSEP_OK;
 }
@@ -212,7 +292,10 @@ int big_block(kvsep_crc32c_ctx* c, HostStaging& s, SlotJob* jobs, uint32_t* out,
   for (uint64_t done = 0; done < n; done += s.bytes, slot ^= 1) {
     const uint64_t seg = std::min<uint64_t>(s.bytes, n - done);
     KVSEP_HIPH(hipEventSynchronize(s.done[slot]));  // previous use of this slot's buffers finished
-    if (!pinned) std::memcpy(s.h_data[slot], p + done, seg);
+    if (!pinned) {
+      const CopySeg cs{s.h_data[slot], p + done, seg};
+      copy_pool_run(s.pool, &cs, 1);
+    }
     s.h_desc[slot][0] = 0;
     s.h_desc[slot][s.max_blocks] = seg;
     hipStream_t st = s.stream[0];
@@ -348,7 +431,10 @@ int kvsep_crc32c_batch_host_span(kvsep_crc32c_ctx* c, const char* host_base, uin
       s.h_desc[slot][s.max_blocks + k] = len[i + k];
       if (init) s.h_init[slot][k] = init[i + k];
     }
-    if (!pinned) std::memcpy(s.h_data[slot], base + lo, hi - lo);
+    if (!pinned) {
+      const CopySeg cs{s.h_data[slot], base + lo, hi - lo};
+      copy_pool_run(s.pool, &cs, 1);
+    }
     rc = submit(c, s, slot, nblk, hi - lo, max_len, pinned ? base + lo : nullptr, init != nullptr);
     if (rc) return rc;
     jobs[slot].busy = true;
@@ -390,11 +476,12 @@ int kvsep_crc32c_batch_host(kvsep_crc32c_ctx* c, const uint32_t* init, const cha
     rc = retire(s, slot, jobs[slot], out);
     if (rc) return rc;
     uint64_t used = 0, j = i, max_len = 0;
-    // gather: blocks packed back to back, each at a 16-B aligned staging offset
+    // gather: blocks packed back to back, each at a 16-B aligned staging offset (copied by the pool below)
+    std::vector<CopySeg> segs;
     while (j < count && j - i < s.max_blocks && len[j] <= s.bytes) {
       const uint64_t at = (used + 15) & ~uint64_t(15);
       if (at + len[j] > s.bytes) break;
-      if (len[j]) std::memcpy(s.h_data[slot] + at, ptr[j], len[j]);
+      if (len[j]) segs.push_back({s.h_data[slot] + at, reinterpret_cast<const uint8_t*>(ptr[j]), len[j]});
       s.h_desc[slot][j - i] = at;
       s.h_desc[slot][s.max_blocks + (j - i)] = len[j];
       if (init) s.h_init[slot][j - i] = init[j];
@@ -402,6 +489,7 @@ int kvsep_crc32c_batch_host(kvsep_crc32c_ctx* c, const uint32_t* init, const cha
       used = at + len[j];
       ++j;
     }
+    copy_pool_run(s.pool, segs.data(), segs.size());
     rc = submit(c, s, slot, j - i, used, max_len, nullptr, init != nullptr);
     if (rc) return rc;
     jobs[slot].busy = true;

@@ -33,6 +33,18 @@ struct Scratch {
 };
 void free_scratch(Scratch& sc);
 
+// Persistent host threads that copy pageable data into the pinned staging slots in parallel: one thread's
+// memcpy (~10-25 GB/s) is below the PCIe Gen5 x16 rate the slots are drained at (~55 GB/s).
+class CopyPool;
+struct CopySeg {
+  uint8_t* dst;
+  const uint8_t* src;
+  uint64_t n;
+};
+CopyPool* copy_pool_create();
+void copy_pool_destroy(CopyPool* p);
+void copy_pool_run(CopyPool* p, const CopySeg* segs, uint64_t nseg);  // returns when every byte is copied
+
 // Double-buffered host<->device staging for the host-memory entry points.
 struct HostStaging {
   static constexpr int kSlots = 2;
@@ -49,6 +61,7 @@ struct HostStaging {
   hipStream_t stream[kSlots] = {nullptr, nullptr};
   hipEvent_t done[kSlots] = {nullptr, nullptr};
   Scratch scratch[kSlots];
+  CopyPool* pool = nullptr;
   bool ready = false;
 };
 
