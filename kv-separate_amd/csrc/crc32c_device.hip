@@ -862,30 +862,30 @@ __global__ void fill_splitmix_bytes_kernel(uint8_t* dst, uint64_t n, uint64_t se
   }
 }
 
-// The attainable-read ceiling for the same access pattern as the CRC kernel: each wave streams its own
-// contiguous 1 MiB chunk as 1 KiB rows with non-temporal loads.  Launched as 2 x 512-thread workgroups per CU
-// with 16 rows in flight per wave: the best of tools/hbm_probe's sweep (7.08 TB/s on 64 GiB; 8 rows 7.03-7.06,
-// 4 rows 6.95).
-constexpr int kStreamRows = 16;
+// The attainable-read ceiling: the fastest read-only streaming pattern of tools/hbm_probe.hip's sweeps.  Each
+// 8-wave workgroup owns a contiguous 1 MiB chunk at a time and its waves read interleaved 1 KiB rows (wave w:
+// rows w, w+8, ...), 8 rows in flight per wave, non-temporal loads, one workgroup per CU: 7.17-7.22 TB/s on
+// 64 GiB, against 6.9-7.1 for per-wave chunks at 16 rows in flight and 6.3 for plain loads.
+constexpr int kStreamRows = 8;
 __global__ void __launch_bounds__(512) stream_read_kernel(uintptr_t src, uint64_t n16, uint32_t* sink) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t wave = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
-  const uint64_t nwaves = (uint64_t(gridDim.x) * blockDim.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   constexpr uint64_t kChunk16 = (1u << 20) / 16;
+  constexpr uint64_t kStep = 8 * kStreamRows * kRowBytes;  // bytes per round of the workgroup
   const uint64_t nchunks = n16 / kChunk16;
   uint32_t acc = 0;
-  for (uint64_t c = wave; c < nchunks; c += nwaves) {
-    const uintptr_t p = src + (c * kChunk16 + lane) * 16;
-    for (uint64_t r = 0; r < kChunk16 * 16; r += kStreamRows * kRowBytes) {
+  for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const uintptr_t p = src + c * kChunk16 * 16 + uintptr_t(w) * kRowBytes + lane * 16u;
+#pragma unroll 1  // one round at a time: software-pipelining rounds (16 rows in flight) measured 5 % slower
+    for (uint64_t r = 0; r < kChunk16 * 16; r += kStep) {
       uint4 v[kStreamRows];
 #pragma unroll
-      for (int u = 0; u < kStreamRows; ++u) v[u] = ld16<true>(p + r + u * kRowBytes);
-      __builtin_amdgcn_sched_barrier(0);  // all 16 rows in flight before any use (no register-reuse waits)
+      for (int u = 0; u < kStreamRows; ++u) v[u] = ld16<true>(p + r + uint64_t(u) * 8 * kRowBytes);
 #pragma unroll
       for (int u = 0; u < kStreamRows; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
     }
   }
-  for (uint64_t i = nchunks * kChunk16 + wave * 64 + lane; i < n16; i += nwaves * 64) {
+  const uint64_t nthreads = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = nchunks * kChunk16 + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n16; i += nthreads) {
     const uint4 x = ld16<true>(src + i * 16);
     acc ^= x.x ^ x.y ^ x.z ^ x.w;
   }
@@ -1425,7 +1425,7 @@ int kvsep_stream_read_device(kvsep_crc32c_ctx* c, void* stream, const void* src,
     e1 = take_event(c);
     if (e0 && e1) KVSEP_HIP(hipEventRecord(e0, s));
   }
-  stream_read_kernel<<<unsigned(2 * c->num_cus), 512, 0, s>>>(reinterpret_cast<uintptr_t>(src), n16, sink);
+  stream_read_kernel<<<unsigned(c->num_cus), 512, 0, s>>>(reinterpret_cast<uintptr_t>(src), n16, sink);
   KVSEP_HIP(hipGetLastError());
   if (c->timing && e0 && e1) {
     KVSEP_HIP(hipEventRecord(e1, s));
