@@ -12,6 +12,8 @@ cp $O/prof/stats_kernel_stats.csv $D/kernel_stats_cfg3a.csv
 cp $O/prof/stats_kernel_trace.csv $D/kernel_trace_cfg3a.csv
 cp $O/kernel_trace_cfg3a.json $D/kernel_trace_cfg3a.json
 cp $O/prof.json $D/bench_under_rocprof_cfg3a.json
+cp $O/prof2/stats_kernel_stats.csv $D/kernel_stats_cfg2.csv
+cp $O/kernel_trace_cfg2.json $D/kernel_trace_cfg2.json
 for c in 3a 3b 4 2; do
   cp $O/pmc_cfg$c.json $D/pmc_cfg$c.json
   cp $O/pmc_cfg$c.json $R/profiles/pmc_cfg$c.json
