@@ -390,8 +390,8 @@ __device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* rep, cons
   }
 }
 
-// kThreads: 1024 (16 waves, 4 per SIMD, <= 128 VGPRs) or 768 (12 waves, 3 per SIMD, <= 168 VGPRs: room for
-// deeper row groups).  One workgroup per CU either way (the LDS image is 157 KiB).
+// kThreads: 512 (8 waves, 2 per SIMD, <= 256 VGPRs; the default), 768, 1024 or 256 for A/B (launch_pieces_v).
+// One workgroup per CU in every case (the LDS image is 157 KiB).
 template <bool kPlanned, bool kDynamic, int kG, bool kNT, bool kAhead, int kAbl = 0, int kThreads = kWgThreads>
 __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
@@ -579,7 +579,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Narrow kernel for batches of short blocks (every block <= kNarrowMax): a wavefront runs 8 blocks at once,
+// Narrow kernel for batches of many short blocks (use_narrow): a wavefront runs 8 blocks at once,
 // kNarrowLanes = 8 lanes ("a slot") per block and rows of 128 B ending at the block's aligned end.  The wide
 // kernel pays a fixed cost per block (lane merge, 6-level lane tree, staging: ~230 of its ~313 VALU
 // instructions for a 4 KiB block, PMC SQ_INSTS_VALU); here the merge is a 3-level tree inside the slot and
@@ -696,7 +696,7 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
   return reg;
 }
 
-// Unsplit batches only (every block <= kNarrowMax <= piece_bytes); static contiguous runs of 8-block groups.
+// Unsplit batches only (every block <= 64 KiB <= piece_bytes); static contiguous runs of 8-block groups.
 template <int kG, bool kNT, int kThreads>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
@@ -1158,7 +1158,7 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     a.work_counter = sc.d_counter;
     KVSEP_HIP(hipMemsetAsync(sc.d_counter, 0, 4, s));
   }
-  const unsigned grid = unsigned(c->num_cus);  // one 16-wave workgroup per CU, persistent
+  const unsigned grid = unsigned(c->num_cus);  // one workgroup per CU, persistent
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->timing) {
     e0 = take_event(c);
