@@ -118,8 +118,8 @@ def cpu_baseline(oracle, data_dev, off, ln, sample_blocks, threads, seconds):
     return out, host, hoff, lens, idx, kind
 
 
-def host_roundtrip(ctx, nbytes_target: int):
-    """Pinned host vlog image -> H2D -> CRC kernel -> D2H of the u32 results (two streams)."""
+def roundtrip_setup(ctx, nbytes_target: int):
+    """A pinned host vlog image (config 3b records) and its device-resident reference results."""
     off, ln = W.cfg3_layout(vlog=True, count=max(1, nbytes_target // (W.VLOG_PAYLOAD + 8)))
     span = int(off[-1] + ln[-1])
     buf = torch.empty(span, dtype=torch.uint8, pin_memory=True)
@@ -134,12 +134,16 @@ def host_roundtrip(ctx, nbytes_target: int):
     del dev
     arr = buf.numpy()
     ctx.batch_host_span(arr, off, ln)  # warm staging
+    return buf, arr, off, ln, ref
+
+
+def roundtrip_time(ctx, state, reps=3):
+    """Pinned host image -> H2D -> CRC kernel -> D2H of the u32 results (two streams): seconds per pass."""
+    _, arr, off, ln, ref = state
     t0 = time.perf_counter()
-    reps = 3
     for _ in range(reps):
         res = ctx.batch_host_span(arr, off, ln)
-    dt = (time.perf_counter() - t0) / reps
-    return float(ln.sum()) / GIB / dt, int(ln.sum()), bool(np.array_equal(res, ref))
+    return (time.perf_counter() - t0) / reps, bool(np.array_equal(res, ref))
 
 
 def main():
@@ -310,14 +314,31 @@ def main():
             exp = [oracle.extend_addr(0, h.ctypes.data, h.size) for h in hostb]
             parity = bool(list(crcs[idx]) == exp)
 
+    # host round trip (PCIe-inclusive).  At N > 1 every rank streams its own pinned image through its own GPU
+    # at the same time (each GPU has its own PCIe link); the rate is the sum over ranks / the slowest rank.
+    # Every rank runs the same collectives whatever fails locally, so a failure cannot leave a rank waiting.
     rt = None
     rt_ok = None
-    if rank == 0 and world == 1 and args.roundtrip_gib > 0:
+    if args.roundtrip_gib > 0:
+        dd = dist if world > 1 else None
+        state = None
         try:
-            rt_gibps, rt_bytes, rt_ok = host_roundtrip(ctx, int(args.roundtrip_gib * GIB))
-            rt = round(rt_gibps, 3)
+            state = roundtrip_setup(ctx, int(args.roundtrip_gib * GIB))
         except Exception as e:  # keep the headline line even if pinned allocation is refused
-            log(f"host round trip failed: {e}")
+            log(f"[rank {rank}] host round trip setup failed: {e}")
+        if shard.min_over_ranks(1 if state is not None else 0, dd, coll_dev):
+            if world > 1:
+                dist.barrier()
+            dt, good = float("inf"), False
+            try:
+                dt, good = roundtrip_time(ctx, state)
+            except Exception as e:
+                log(f"[rank {rank}] host round trip failed: {e}")
+            dt = shard.max_over_ranks(dt, dd, coll_dev)
+            rt_ok = bool(shard.min_over_ranks(1 if good else 0, dd, coll_dev))
+            if dt != float("inf"):
+                rt = round(world * float(state[3].sum()) / GIB / dt, 3)
+        state = None
 
     traffic = None
     pmc_cfg = "3b" if args.config == "5" else args.config  # config 5's launches are config-3b launches
@@ -357,6 +378,7 @@ def main():
             "read_ceiling_GBps": read_ceiling_gbps and round(read_ceiling_gbps, 1),
             "frac_of_read_ceiling": read_ceiling_gbps and round(achieved_gbps / read_ceiling_gbps, 4),
             "host_roundtrip_GiBps": rt,
+            "host_roundtrip_ranks": world if rt is not None else None,
             "host_roundtrip_parity": rt_ok,
             "parity_spot_check": parity,
             "digests": [hex(d) for d in digests],

@@ -39,6 +39,16 @@ def max_over_ranks(value: float, dist, device) -> float:
     return float(t.item())
 
 
+def min_over_ranks(value: float, dist, device) -> float:
+    import torch
+
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return float(t.item())
+
+
 def gather_digests(digest: int, dist, device) -> list[int]:
     """All-gather one 32-bit digest per rank (the only result traffic between GPUs)."""
     import torch

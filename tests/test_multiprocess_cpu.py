@@ -41,6 +41,7 @@ def _worker(rank, world, port, q):
     crcs = np.array([kvsep.extend_host(0, data[int(o):int(o + l)]) for o, l in zip(off, ln)], dtype=np.uint32)
     digests = shard.gather_digests(shard.crc_of_crcs(crcs, kvsep.extend_host), dist, dev)
     elapsed = shard.max_over_ranks(0.5 + rank, dist, dev)
+    assert shard.min_over_ranks(0.5 + rank, dist, dev) == 0.5
     # verify mode: rank 1 sees a corrupted record 7 (global index COUNT + 7)
     expected = np.array([kvsep.mask(int(c)) for c in crcs], np.uint32)
     if rank == 1:
