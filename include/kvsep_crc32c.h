@@ -78,7 +78,8 @@ const char* kvsep_crc32c_kernel_name(kvsep_crc32c_ctx* ctx, uint64_t count, uint
  * base/off/len/init/out are DEVICE pointers; the call is asynchronous on `stream`
  * (a hipStream_t; NULL = default stream).  Blocks may overlap and sit at any byte alignment.
  * total_bytes >= sum(len) (sizes scratch only); max_len = an upper bound on len[i] or 0 if unknown
- * (when max_len <= piece size the planning pass is skipped).  count <= 2^32 - 1 (else KVSEP_EINVAL). */
+ * (when max_len <= piece size the planning pass is skipped; a max_len that is not an upper bound gives
+ * undefined results).  count <= 2^32 - 1 (else KVSEP_EINVAL). */
 int kvsep_crc32c_batch_device(kvsep_crc32c_ctx* ctx, void* stream, const void* base, const uint64_t* off,
                               const uint64_t* len, const uint32_t* init, uint32_t* out, uint64_t count,
                               uint64_t total_bytes, uint64_t max_len);
