@@ -442,10 +442,10 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
     } else if (a.static_contig) {
       if (lo != ~uint64_t(0)) return false;
       const uint64_t per = (total + nwaves - 1) / nwaves;
-      lo = (uint64_t(blockIdx.x) * kWavesPerWg + wave) * per;
+      lo = (uint64_t(wave) * gridDim.x + blockIdx.x) * per;  // wave-major: see the narrow kernel
       hi = lo + per < total ? lo + per : total;
     } else {
-      lo = (lo == ~uint64_t(0)) ? uint64_t(blockIdx.x) * kWavesPerWg + wave : lo + nwaves;
+      lo = (lo == ~uint64_t(0)) ? uint64_t(wave) * gridDim.x + blockIdx.x : lo + nwaves;
       hi = lo + 1;
     }
     return lo < total;
@@ -712,10 +712,11 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   const uintptr_t dummy = reinterpret_cast<uintptr_t>(a.tabs);
   constexpr uint32_t kPerGroup = 64 / kNarrowLanes;
 
-  // contiguous run of whole groups per wave
+  // contiguous run of whole groups per wave.  Runs are numbered wave-major (run w*grid + b), so when there are
+  // fewer groups than waves the busy waves are spread over every CU instead of filling the first CUs.
   const uint64_t groups = (a.count + kPerGroup - 1) / kPerGroup;
   const uint64_t gper = (groups + nwaves - 1) / nwaves;
-  const uint64_t lo = (uint64_t(blockIdx.x) * kWavesPerWg + wave) * gper * kPerGroup;
+  const uint64_t lo = (uint64_t(wave) * gridDim.x + blockIdx.x) * gper * kPerGroup;
   uint64_t hi = lo + gper * kPerGroup;
   if (hi > a.count) hi = a.count;
 
