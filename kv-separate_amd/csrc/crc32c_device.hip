@@ -1003,8 +1003,9 @@ int ensure_plan(Scratch& sc, uint64_t piece_bytes, uint64_t count, uint64_t tota
 // Narrow or wide kernel for an unsplit batch (every block <= piece_bytes, known from the max_len hint)?  The
 // narrow kernel's unit of parallelism is an 8-block group, so it needs many blocks; it wins on short blocks
 // when there are enough of them (measured, tools/ab_variants.py on one MI355X):
-//   <= 8 KiB blocks from 16 Ki blocks up (1 M x 4 KiB: 6.67 vs 3.7 TB/s; 4 Ki x 4 KiB: the wide kernel wins),
-//   <= 32 KiB blocks from 32 Ki blocks up (32 Ki x 16 KiB: 6.05 vs 5.94; 16 Ki x 32 KiB: wide 6.25 vs 5.25),
+//   <= 8 KiB blocks from 8 Ki blocks up (8 Ki x 4 KiB: 2.58 vs 2.13 TB/s; 4 Ki x 4 KiB: wide 1.50 vs 1.46),
+//   <= 16 KiB blocks from 16 Ki blocks up (16 Ki x 16 KiB: 5.58 vs 5.36; 4 Ki x 16 KiB: wide 3.67 vs 2.58),
+//   <= 32 KiB blocks from 32 Ki blocks up (32 Ki x 32 KiB: 6.72 vs 6.35; 16 Ki x 32 KiB: wide 6.12 vs 6.06),
 //   64 KiB blocks never (16 Ki x 64 KiB: wide 6.22 vs 4.88).
 // The thresholds scale with the CU count (256 on MI355X).
 // KVSEP_NARROW: 0 never, 1 this rule (default), 2..7 always when max_len <= 64 KiB (tests, A/B).
@@ -1012,7 +1013,8 @@ bool use_narrow(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t max_len) {
   if (!c->narrow || max_len == 0) return false;
   if (c->narrow >= 2) return max_len <= 2 * kNarrowMax;
   const uint64_t cus = uint64_t(c->num_cus);
-  return (max_len <= 8 * 1024 && count >= 64 * cus) || (max_len <= kNarrowMax && count >= 128 * cus);
+  return (max_len <= 8 * 1024 && count >= 32 * cus) || (max_len <= 16 * 1024 && count >= 64 * cus) ||
+         (max_len <= kNarrowMax && count >= 128 * cus);
 }
 
 // Piece size of a planned batch.  With the default setting, a batch too small to give every wave two pieces
@@ -1165,11 +1167,13 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     if (e0 && e1) KVSEP_HIP(hipEventRecord(e0, s));
   }
   if (!planned && use_narrow(c, count, max_len)) {
-    // 1 (default): 16-wave workgroups below 128 Ki blocks, 8-wave ones from there on.  A small batch gives each
-    // wave only a couple of 8-block groups, and more waves hide more of the launch/first-load ramp (256 MiB
-    // of 4 KiB blocks: 16 waves +5 %); a large one streams better with 8 (4 GiB of 4 KiB blocks: +3 %).
+    // 1 (default): 16-wave workgroups below 128 Ki blocks of <= 8 KiB (32 Ki blocks of 8-32 KiB), 8-wave ones
+    // from there on.  A small batch gives each wave only a couple of 8-block groups, and more waves hide more of
+    // the launch/first-load ramp (256 MiB of 4 KiB blocks: 16 waves +2-5 %); a large one streams better with 8
+    // (1 GiB of 4 KiB blocks: +5 %; 32 Ki x 16 KiB +2 %, 32 Ki x 32 KiB +6 %).
     // 2: always 8 waves; 3: 12 waves; 4 / 5: 8-row groups at 8 / 12 waves; 6: always 16 waves; 7: as 1.
-    const int nv = (c->narrow == 1 || c->narrow == 7) ? (count >= (1u << 17) ? 2 : 6) : c->narrow;
+    const bool eight_waves = max_len <= 8 * 1024 ? count >= (1u << 17) : count >= (1u << 15);
+    const int nv = (c->narrow == 1 || c->narrow == 7) ? (eight_waves ? 2 : 6) : c->narrow;
     switch (nv) {
       case 2: crc32c_narrow_kernel<4, true, 512><<<grid, 512, 0, s>>>(a); break;
       case 3: crc32c_narrow_kernel<4, true, 768><<<grid, 768, 0, s>>>(a); break;
