@@ -18,6 +18,7 @@ import ctypes
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -116,6 +117,47 @@ def cpu_baseline(oracle, data_dev, off, ln, sample_blocks, threads, seconds):
                 break
         out[t] = (passes * sb / GIB / dt, passes * sb, dt)
     return out, host, hoff, lens, idx, kind
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def sse42_rate(host, hoff, lens, threads, seconds):
+    """Informational: the library's own SSE4.2 `crc32` host leg (the drop-in's small-input path, i.e. the
+    "accelerated" CPU path google/crc32c would give the reference) over the same host sample; GiB/s."""
+    fn = kvsep.lib().kvsep_crc32c_extend_host
+    base = host.ctypes.data
+    items = [(base + int(o), int(n)) for o, n in zip(hoff, lens)]
+    parts = [items[t::threads] for t in range(threads)]
+    total = sum(n for _, n in items)
+    fn(0, items[0][0], min(items[0][1], 4096))  # warm
+
+    def work(part, stop_at, acc):
+        while True:
+            for a, n in part:
+                fn(0, a, n)
+            acc.append(sum(n for _, n in part))
+            if time.perf_counter() >= stop_at:
+                return
+
+    t0 = time.perf_counter()
+    accs = [[] for _ in range(threads)]
+    ths = [threading.Thread(target=work, args=(parts[t], t0 + seconds, accs[t])) for t in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t0
+    done = sum(sum(a) for a in accs)
+    return done / GIB / dt, total
 
 
 def roundtrip_setup(ctx, nbytes_target: int):
@@ -307,7 +349,13 @@ def main():
                              f"memory, {impl_desc}; {threads} threads split by bytes: {sbt / GIB:.1f} GiB in "
                              f"{dtt:.1f} s (repeated passes); 1 thread: {v1:.3f} GiB/s, {sb1 / GIB:.1f} GiB in "
                              f"{dt1:.1f} s",
-                   "single_thread_GiBps": round(v1, 3)}
+                   "single_thread_GiBps": round(v1, 3), "cpu_model": cpu_model()}
+            s1, _ = sse42_rate(host, hoff[:max(1, nsample // 4)], lens[:max(1, nsample // 4)], 1, 2.0)
+            sn, _ = sse42_rate(host, hoff, lens, threads, 2.0)
+            cpu["sse42_crc32_GiBps"] = {"1": round(s1, 3), str(threads): round(sn, 3),
+                                        "note": "informational, not the baseline: the library's SSE4.2 crc32 host "
+                                                "leg (3-way interleaved crc32q) on the same sample; the reference "
+                                                "build here has no accelerated path (HAVE_CRC32C=0)"}
         else:
             idx = np.linspace(0, count - 1, 16).astype(np.int64)
             hostb = [data[int(off[i]):int(off[i] + ln[i])].cpu().numpy() for i in idx]
