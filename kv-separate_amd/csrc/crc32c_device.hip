@@ -4,7 +4,7 @@
 // blocks resident in HBM.  Design:
 //
 //  * Work item = "piece": a block, or an end-aligned slice of at most `piece_bytes` of a long block
-//    (pieces 1..k-1 are exactly piece_bytes long, piece 0 takes the remainder and the init CRC).
+//    (pieces 1..k-1 are exactly piece_bytes long, piece 0 takes the remainder on top of a full piece, and the init CRC).
 //  * One wavefront per piece.  The piece is cut at 16-byte-aligned addresses into
 //      head  [ps, h0)   < 16 B, serial (word/byte steps),
 //      body  [h0, a1)   16-B aligned, as rows of 1 KiB ending exactly at a1,
@@ -805,7 +805,10 @@ __global__ void crc32c_plan_count_kernel(const uint64_t* len, uint64_t count, ui
   const uint64_t b = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (b >= count) return;
   const uint64_t n = len[b];
-  counts[b] = n <= piece_bytes ? 1u : uint32_t((n + piece_bytes - 1) / piece_bytes);
+  // floor, not ceil: piece 0 takes the remainder ON TOP of a full piece (length in [P, 2P)), so no block ends
+  // up with a short remainder piece that costs a work item of its own (3b: 33-B pieces, one per record);
+  // only the later pieces must be exactly P long for the combine's Z_P.
+  counts[b] = n < 2 * piece_bytes ? 1u : uint32_t(n / piece_bytes);
 }
 
 // SST write side (table/table_builder.cc:222-225): crc = Extend(Value(block), &type, 1); trailer word = Mask(crc).

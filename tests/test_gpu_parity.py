@@ -168,6 +168,31 @@ def test_random_blocks_many_pieces_vs_oracle(ctx, oracle):
     ctx.set_piece_bytes(kvsep.DEFAULT_PIECE_BYTES)
 
 
+@pytest.mark.parametrize("piece", [1024, 4096, 128 * 1024])
+def test_piece_count_boundaries(ctx, oracle, piece):
+    """Blocks at every length class of the piece plan (crc32c_plan_count_kernel: k = 1 below 2P, else
+    floor(n / P), piece 0 = n - (k-1) P in [P, 2P)): P-1 .. 2P+1, kP +- 1, at odd offsets, both schedules."""
+    P = piece
+    lens = []
+    for k in (1, 2, 3, 5):
+        lens += [k * P - 1, k * P, k * P + 1, k * P + 33]
+    lens += [2 * P - 16, 2 * P + 15, 0, 1, 15, 16, 17]
+    ln = np.array(lens * 3, dtype=np.uint64)
+    data = splitmix64_bytes(int(ln.sum()) + 64 * ln.size + 64, 1234, 0)
+    off = (np.cumsum(ln + np.uint64(3)) - ln).astype(np.uint64)  # ragged odd-ish offsets
+    init = np.arange(ln.size, dtype=np.uint32) * np.uint32(2654435761)
+    exp = oracle.batch(data, off, ln, init, threads=8)
+    d = dev_bytes(data)
+    ctx.set_piece_bytes(P)
+    try:
+        for dyn in (False, True):
+            ctx.set_schedule(dyn)
+            assert np.array_equal(run(ctx, d, off, ln, init), exp), dyn
+    finally:
+        ctx.set_piece_bytes(kvsep.DEFAULT_PIECE_BYTES)
+        ctx.set_schedule(None)
+
+
 def test_edge_cases(ctx):
     d = dev_bytes(splitmix64_bytes(4096, 3, 0))
     # empty batch is a no-op
