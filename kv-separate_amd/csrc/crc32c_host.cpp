@@ -333,6 +333,24 @@ kvsep_crc32c_ctx* default_ctx() {
 }
 
 }  // namespace
+
+// Parallel host copies for the framing writers (payloads into the framed image), on the context's copier
+// pool; a serial memcpy when the pool cannot be set up.  Declared in framing.cpp.
+int host_copy_parallel(kvsep_crc32c_ctx* c, char* const* dst, const char* const* src, const uint64_t* n,
+                       uint64_t count) {
+  std::vector<CopySeg> segs;
+  segs.reserve(count);
+  for (uint64_t i = 0; i < count; ++i)
+    if (n[i]) segs.push_back({reinterpret_cast<uint8_t*>(dst[i]), reinterpret_cast<const uint8_t*>(src[i]), n[i]});
+  std::lock_guard<std::mutex> g(ctx_mutex(c));
+  if (ensure_staging(c) != KVSEP_OK || !ctx_staging(c).pool) {
+    for (auto& sg : segs) std::memcpy(sg.dst, sg.src, sg.n);
+    return KVSEP_OK;
+  }
+  copy_pool_run(ctx_staging(c).pool, segs.data(), segs.size());
+  return KVSEP_OK;
+}
+
 }  // namespace kvsep
 
 using namespace kvsep;

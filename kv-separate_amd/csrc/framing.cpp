@@ -12,9 +12,16 @@
 // The serial parts (header walks) stay on the host; every checksum goes through one batched call.
 #include <cstdint>
 #include <cstring>
+#include <utility>
 #include <vector>
 
 #include "../../include/kvsep_crc32c.h"
+
+namespace kvsep {
+// crc32c_host.cpp: copies dst[i] <- src[i] (n[i] bytes) on the context's copier threads.
+int host_copy_parallel(kvsep_crc32c_ctx* c, char* const* dst, const char* const* src, const uint64_t* n,
+                       uint64_t count);
+}  // namespace kvsep
 
 namespace {
 
@@ -92,13 +99,14 @@ int kvsep_vlog_frame_host(kvsep_crc32c_ctx* ctx, const char* const* payload, con
     if (rc) return rc;
   }
   uint64_t p = 0;
+  std::vector<char*> at(count);
   for (uint64_t i = 0; i < count; ++i) {  // db/value_log_writer.cc:57-70
     put_le32(dst + p, kvsep_crc32c_mask(crc[i]));
     put_le32(dst + p + 4, uint32_t(len[i]));
-    if (len[i]) std::memcpy(dst + p + kVlogHeader, payload[i], len[i]);
+    at[i] = dst + p + kVlogHeader;
     p += kVlogHeader + len[i];
   }
-  return KVSEP_OK;
+  return kvsep::host_copy_parallel(ctx, at.data(), payload, len, count);  // the payload bytes
 }
 
 uint64_t kvsep_log_walk(const char* buf, uint64_t n, uint64_t* off, uint64_t* len, uint32_t* stored, uint8_t* type,
@@ -152,6 +160,7 @@ int kvsep_log_frame_host(kvsep_crc32c_ctx* ctx, const char* const* payload, cons
     uint8_t type;
   };
   std::vector<Frag> frags;
+  std::vector<std::pair<uint64_t, uint64_t>> trailers;  // zero-filled block ends [at, at + n)
   uint64_t block_offset = dest_length % kLogBlock, p = 0;
   for (uint64_t r = 0; r < count; ++r) {  // log::Writer::AddRecord (:35-82)
     const char* ptr = payload[r];
@@ -160,6 +169,7 @@ int kvsep_log_frame_host(kvsep_crc32c_ctx* ctx, const char* const* payload, cons
     do {
       const uint64_t leftover = kLogBlock - block_offset;
       if (leftover < kLogHeader) {  // trailer: zero-filled, next block (:48-57)
+        if (leftover) trailers.emplace_back(p, leftover);
         p += leftover;
         block_offset = 0;
       }
@@ -195,16 +205,17 @@ int kvsep_log_frame_host(kvsep_crc32c_ctx* ctx, const char* const* payload, cons
     const int rc = kvsep_crc32c_batch_host(ctx, init.data(), src.data(), flen.data(), crc.data(), nf);
     if (rc) return rc;
   }
-  if (p) std::memset(dst, 0, p);  // trailers
+  for (const auto& t : trailers) std::memset(dst + t.first, 0, t.second);
+  std::vector<char*> at(nf);
   for (uint64_t i = 0; i < nf; ++i) {  // EmitPhysicalRecord (:84-115)
     char* h = dst + frags[i].at;
     put_le32(h, kvsep_crc32c_mask(crc[i]));
     h[4] = char(frags[i].len & 0xff);
     h[5] = char(frags[i].len >> 8);
     h[6] = char(frags[i].type);
-    if (frags[i].len) std::memcpy(h + kLogHeader, frags[i].src, frags[i].len);
+    at[i] = h + kLogHeader;
   }
-  return KVSEP_OK;
+  return kvsep::host_copy_parallel(ctx, at.data(), src.data(), flen.data(), nf);  // the fragment bytes
 }
 
 uint64_t kvsep_log_accept(const uint64_t* off, const uint8_t* ok, uint64_t count, uint64_t n, uint8_t* accept) {

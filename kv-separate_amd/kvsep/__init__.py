@@ -308,34 +308,55 @@ class Context:
                                             ctypes.byref(gb)), "kvsep_vlog_verify_host")
         return n.value, g.value, gb.value
 
-    def vlog_frame(self, payloads):
-        """db/value_log_writer.cc:46-76 for a batch of payloads -> bytes of the framed records."""
+    def vlog_frame(self, payloads, out=None):
+        """db/value_log_writer.cc:46-76 for a batch of payloads -> bytes of the framed records; with `out` (a
+        writable uint8 numpy array of >= sum(8 + len) bytes) the records are framed into it and the byte count
+        is returned instead."""
         keep = [_buf(b) for b in payloads]
         k = len(payloads)
         ptrs = (ctypes.c_void_p * max(k, 1))(*[x[0].value for x in keep])
         lens = np.array([x[1].nbytes for x in keep], dtype=np.uint64)
         need = int(lens.sum()) + 8 * k
-        dst = np.zeros(max(need, 1), dtype=np.uint8)
+        dst = np.zeros(max(need, 1), dtype=np.uint8) if out is None else out
         w = ctypes.c_uint64()
         _check(lib().kvsep_vlog_frame_host(self._h, ptrs, lens.ctypes.data_as(ctypes.c_void_p), k,
                                            dst.ctypes.data_as(ctypes.c_void_p), dst.nbytes, ctypes.byref(w)),
                "kvsep_vlog_frame_host")
-        return dst[:w.value].tobytes()
+        return dst[:w.value].tobytes() if out is None else w.value
 
-    def log_frame(self, records, dest_length: int = 0):
-        """db/log_writer.cc:35-115: AddRecord of each record onto a log of length dest_length -> appended bytes."""
+    def log_frame(self, records, dest_length: int = 0, out=None):
+        """db/log_writer.cc:35-115: AddRecord of each record onto a log of length dest_length -> appended bytes;
+        with `out` (a writable uint8 numpy array, large enough) they are written into it and the count returned."""
         keep = [_buf(b) for b in records]
         k = len(records)
         ptrs = (ctypes.c_void_p * max(k, 1))(*[x[0].value for x in keep])
         lens = np.array([x[1].nbytes for x in keep], dtype=np.uint64)
         w = ctypes.c_uint64()
-        lib().kvsep_log_frame_host(self._h, ptrs, lens.ctypes.data_as(ctypes.c_void_p), k, dest_length, None, 0,
-                                   ctypes.byref(w))  # sizing call: *written even when dst is short
-        dst = np.zeros(max(w.value, 1), dtype=np.uint8)
+        if out is None:
+            lib().kvsep_log_frame_host(self._h, ptrs, lens.ctypes.data_as(ctypes.c_void_p), k, dest_length, None, 0,
+                                       ctypes.byref(w))  # sizing call: *written even when dst is short
+        dst = np.zeros(max(w.value, 1), dtype=np.uint8) if out is None else out
         _check(lib().kvsep_log_frame_host(self._h, ptrs, lens.ctypes.data_as(ctypes.c_void_p), k, dest_length,
                                           dst.ctypes.data_as(ctypes.c_void_p), dst.nbytes, ctypes.byref(w)),
                "kvsep_log_frame_host")
-        return dst[:w.value].tobytes()
+        return dst[:w.value].tobytes() if out is None else w.value
+
+    def frame_raw(self, kind: str, addrs, lens, out, dest_length: int = 0) -> int:
+        """The framing writers on prebuilt arrays: addrs = uint64 host addresses of the payloads, lens = their
+        uint64 lengths, out = a writable uint8 numpy array (kind "vlog" or "log").  No per-record Python work,
+        so a caller framing thousands of records pays only the C-ABI call.  Returns the bytes written."""
+        addrs = np.ascontiguousarray(addrs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        w = ctypes.c_uint64()
+        vp = ctypes.c_void_p
+        if kind == "vlog":
+            rc = lib().kvsep_vlog_frame_host(self._h, addrs.ctypes.data_as(vp), lens.ctypes.data_as(vp), lens.size,
+                                             out.ctypes.data_as(vp), out.nbytes, ctypes.byref(w))
+        else:
+            rc = lib().kvsep_log_frame_host(self._h, addrs.ctypes.data_as(vp), lens.ctypes.data_as(vp), lens.size,
+                                            dest_length, out.ctypes.data_as(vp), out.nbytes, ctypes.byref(w))
+        _check(rc, f"kvsep_{kind}_frame_host")
+        return w.value
 
     def log_verify(self, image):
         """db/log_reader.cc:246-259 per physical record of a log/MANIFEST image -> array of 0/1."""

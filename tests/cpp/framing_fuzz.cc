@@ -43,6 +43,14 @@ int kvsep_crc32c_batch_host(kvsep_crc32c_ctx*, const uint32_t* init, const char*
   return KVSEP_OK;
 }
 }
+namespace kvsep {
+int host_copy_parallel(kvsep_crc32c_ctx*, char* const* dst, const char* const* src, const uint64_t* n,
+                       uint64_t count) {
+  for (uint64_t i = 0; i < count; ++i)
+    if (n[i]) std::memcpy(dst[i], src[i], n[i]);
+  return KVSEP_OK;
+}
+}  // namespace kvsep
 
 int main() {
   std::mt19937_64 rng(7);

@@ -47,7 +47,11 @@ def test_vlog_recovery_scan(ctx, oracle):
 
 def test_vlog_group_commit_framing(ctx, oracle):
     pl = _payloads(500, 12, 70000) + [b""]
-    assert ctx.vlog_frame(pl) == vlog_image(pl, oracle)
+    ref = vlog_image(pl, oracle)
+    assert ctx.vlog_frame(pl) == ref
+    out = np.full(len(ref) + 100, 0xEE, dtype=np.uint8)  # into a caller buffer; nothing past the image touched
+    assert ctx.vlog_frame(pl, out=out) == len(ref)
+    assert out[:len(ref)].tobytes() == ref and (out[len(ref):] == 0xEE).all()
 
 
 def test_log_manifest_verify(ctx, oracle):
@@ -78,6 +82,9 @@ def test_log_manifest_write_side(ctx, oracle):
     head, _ = log_image(recs[:23], oracle)
     assert head + ctx.log_frame(recs[23:], dest_length=len(head)) == img
     assert (ctx.log_verify(img) == 1).all()
+    out = np.full(len(img) + 50, 0xEE, dtype=np.uint8)  # a dirty caller buffer: trailers must come out zero
+    assert ctx.log_frame(recs, out=out) == len(img)
+    assert out[:len(img)].tobytes() == img and (out[len(img):] == 0xEE).all()
 
 
 def test_sst_trailers_and_verify(ctx, oracle):
