@@ -355,8 +355,15 @@ __device__ __forceinline__ void emit_block(const PiecesArgs& a, uint64_t b, uint
 
 // LDS image of a CRC workgroup: the replicated fold table `rep` (4 byte-tables) at [0, 128 KiB), then the
 // small tables (Z_4, the tree tables, the byte table) as one contiguous run.
-template <int kThreads = kWgThreads>
-__device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* rep, const DevTables* tabs, uint32_t tid) {
+struct NoMid {
+  __device__ void operator()() const {}
+};
+
+// `mid()` runs between the fill's global loads and its LDS stores (pinned there by sched barriers): loads it
+// issues are younger than the table loads, so the stores wait for the tables only (a counted vmcnt).
+template <int kThreads = kWgThreads, typename Mid = NoMid>
+__device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* rep, const DevTables* tabs, uint32_t tid,
+                                         Mid&& mid = Mid()) {
   // Every global load of the fill is issued before the first LDS store: one L2/HBM round trip per
   // workgroup instead of one per loop trip (the fill is a fixed cost of every launch; it dominates
   // small batches, e.g. 4 KiB-block batches of a few MiB).
@@ -377,6 +384,9 @@ __device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* rep, cons
     const uint32_t q = tid + i * kThreads;
     w[i] = q < (kLdsBytes - kZ4Off) / 16 ? src[q] : make_uint4(0, 0, 0, 0);
   }
+  __builtin_amdgcn_sched_barrier(0);
+  mid();
+  __builtin_amdgcn_sched_barrier(0);
   // 16-B stores: 4 consecutive dwords of the replicated image are 4 copies of one entry
 #pragma unroll
   for (uint32_t i = 0; i < kRep; ++i) {
@@ -697,7 +707,7 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
 }
 
 // Unsplit batches only (every block <= 64 KiB <= piece_bytes); static contiguous runs of 8-block groups.
-template <int kG, bool kNT, int kThreads>
+template <int kG, bool kNT, int kThreads, bool kOverlap = false>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -723,19 +733,19 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   // Descriptors run one group ahead of the staging: taking group g stages its rows from descriptors loaded
   // when group g-8 was taken, then loads those of group g+8 (each lane its slot's block: one 64-B line per
   // array, shared by the slot's 8 lanes), so no descriptor load sits between two groups' row loads.
+  // The raw loaded words are kept and only used at the take, a group later: nothing consumes them right
+  // after the loads, so the compiler's wait for them lands at the take, not behind the loads.
   struct Desc {  // 32-bit length: the narrow kernel runs only under a max_len hint <= 64 KiB (a 64-bit end
-    uintptr_t ps;  // spills at 16 waves)
-    uint32_t len, reg0;
+    uint64_t off;  // spills at 16 waves)
+    uint32_t len, init;
   };
-  auto load_desc = [&](uint64_t g, Desc& d) {  // block g + slot; past hi: an empty slot (loads stay in bounds)
+  auto load_desc = [&](uint64_t g, Desc& d) {  // block g + slot; past hi: loads stay in bounds, take() empties it
     const uint64_t b = g + slot;
     const uint64_t bb = b < hi ? b : hi - 1;
-    const uintptr_t blk = reinterpret_cast<uintptr_t>(a.base) + a.off[bb];
-    const uint32_t n = uint32_t(a.len[bb]);
-    const uint32_t r0 = ~(a.init ? a.init[bb] : 0u);
-    d.ps = b < hi ? blk : dummy;
-    d.len = b < hi ? n : 0u;
-    d.reg0 = r0;
+    d.off = a.off[bb];
+    d.len = reinterpret_cast<const uint32_t*>(a.len + bb)[0];  // low word (LE) only: a dead high word's
+                                                               // register got reused, forcing an early wait
+    d.init = *(a.init ? a.init + bb : &a.tabs->z4[0][0]);  // no init: a word that is 0 (Z_4 of byte 0)
   };
   struct NItem {  // the slot's block is g + slot (g: the group's first block, wave-uniform)
     uint32_t reg0;
@@ -743,8 +753,10 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   };
   Desc dn;  // descriptors of the next group to take
   auto take = [&](uint64_t g, NItem& it, NStaged<kG>& st) {
-    it.reg0 = dn.reg0;
-    nstage<kG, kNT>(st, dn.ps, dn.ps + dn.len, j, dummy);
+    const bool live = g + slot < hi;
+    const uintptr_t ps = live ? reinterpret_cast<uintptr_t>(a.base) + dn.off : dummy;
+    it.reg0 = ~dn.init;
+    nstage<kG, kNT>(st, ps, ps + (live ? dn.len : 0u), j, dummy);
     uint32_t km = 0, kn = ~0u;
 #pragma unroll
     for (uint32_t k = 0; k < kPerGroup; ++k) {
@@ -770,12 +782,26 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   NStaged<kG> S, T;
   // The first group's descriptors are fetched during the LDS fill.  Staging its rows before the fill as well
   // measured 4-7 % slower on 256 MiB-1 GiB batches of 4 KiB blocks: the fill then waits behind them.
-  if (lo < hi) load_desc(lo, dn);
-  fill_lds<kThreads>(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
-  __syncthreads();
+  if (kOverlap) {
+    // descriptors, then the table loads, then the first group's rows: the LDS stores wait for the tables
+    // only, so the first HBM round trip overlaps the fill.  Unconditional (an idle wave stages an empty
+    // group), so the store's wait count is the same on every path.
+    load_desc(lo, dn);
+    fill_lds<kThreads>(lds, &a.tabs->znarrow[0][0], a.tabs, tid, [&]() {
+      take(lo, cur, S);
+      load_desc(lo + kPerGroup, dn);
+    });
+    __syncthreads();
+  } else {
+    if (lo < hi) load_desc(lo, dn);
+    fill_lds<kThreads>(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
+    __syncthreads();
+    if (lo < hi) {
+      take(lo, cur, S);
+      load_desc(lo + kPerGroup, dn);
+    }
+  }
   if (lo < hi) {
-    take(lo, cur, S);
-    load_desc(lo + kPerGroup, dn);
     for (uint64_t g = lo;; g += 2 * kPerGroup) {
       if (!step(g, cur, S, nxt, T)) break;
       if (!step(g + kPerGroup, nxt, T, cur, S)) break;
@@ -1011,7 +1037,7 @@ int ensure_plan(Scratch& sc, uint64_t piece_bytes, uint64_t count, uint64_t tota
 //   <= 32 KiB blocks from 32 Ki blocks up (32 Ki x 32 KiB: 6.72 vs 6.35; 16 Ki x 32 KiB: wide 6.12 vs 6.06),
 //   64 KiB blocks never (16 Ki x 64 KiB: wide 6.22 vs 4.88).
 // The thresholds scale with the CU count (256 on MI355X).
-// KVSEP_NARROW: 0 never, 1 this rule (default), 2..7 always when max_len <= 64 KiB (tests, A/B).
+// KVSEP_NARROW: 0 never, 1 this rule (default), 2..7, 9 always when max_len <= 64 KiB (tests, A/B).
 bool use_narrow(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t max_len) {
   if (!c->narrow || max_len == 0) return false;
   if (c->narrow >= 2) return max_len <= 2 * kNarrowMax;
@@ -1173,15 +1199,17 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     // 1 (default): 16-wave workgroups below 128 Ki blocks of <= 8 KiB (32 Ki blocks of 8-32 KiB), 8-wave ones
     // from there on.  A small batch gives each wave only a couple of 8-block groups, and more waves hide more of
     // the launch/first-load ramp (256 MiB of 4 KiB blocks: 16 waves +2-5 %); a large one streams better with 8
-    // (1 GiB of 4 KiB blocks: +5 %; 32 Ki x 16 KiB +2 %, 32 Ki x 32 KiB +6 %).
-    // 2: always 8 waves; 3: 12 waves; 4 / 5: 8-row groups at 8 / 12 waves; 6: always 16 waves; 7: as 1.
+    // (1 GiB of 4 KiB blocks: +5 %; 32 Ki x 16 KiB +2 %, 32 Ki x 32 KiB +6 %).  The 8-wave kernel overlaps the
+    // LDS fill with the first group's loads (9; +0.3-2 % over 2); at 16 waves that overlap measured -5 %.
+    // 2: always 8 waves; 3: 12 waves; 4 / 5: 8-row groups at 8 / 12 waves; 6: always 16 waves; 7: as 1; 9: 8 waves, fill overlapped with the first loads.
     const bool eight_waves = max_len <= 8 * 1024 ? count >= (1u << 17) : count >= (1u << 15);
-    const int nv = (c->narrow == 1 || c->narrow == 7) ? (eight_waves ? 2 : 6) : c->narrow;
+    const int nv = (c->narrow == 1 || c->narrow == 7) ? (eight_waves ? 9 : 6) : c->narrow;
     switch (nv) {
       case 2: crc32c_narrow_kernel<4, true, 512><<<grid, 512, 0, s>>>(a); break;
       case 3: crc32c_narrow_kernel<4, true, 768><<<grid, 768, 0, s>>>(a); break;
       case 4: crc32c_narrow_kernel<8, true, 512><<<grid, 512, 0, s>>>(a); break;
       case 5: crc32c_narrow_kernel<8, true, 768><<<grid, 768, 0, s>>>(a); break;
+      case 9: crc32c_narrow_kernel<4, true, 512, true><<<grid, 512, 0, s>>>(a); break;
       default: crc32c_narrow_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
     }
   } else {

@@ -79,7 +79,7 @@ def test_wide_variant_ragged(ragged, variant):
         ctx.close()
 
 
-@pytest.mark.parametrize("narrow", ["1", "2", "3", "4", "5", "6", "7"])
+@pytest.mark.parametrize("narrow", ["1", "2", "3", "4", "5", "6", "7", "9"])
 def test_narrow_variant_ragged(ragged, narrow):
     d, off, ln, init, exp = ragged
     ctx = make_ctx("1", narrow)
