@@ -21,9 +21,11 @@ from kvsep import workloads as W  # noqa: E402
 
 
 def layout(cfg):
-    if cfg.startswith("u"):  # "u<count>x<len>": uniform packed blocks, e.g. u4096x4096
-        count, length = cfg[1:].split("x")
-        return W.uniform_layout(int(count), int(length))
+    if cfg.startswith("u"):  # "u<count>x<len>[s<stride>][f<first>]": uniform blocks (packed unless s), e.g. u4096x4096
+        import re
+        m = re.fullmatch(r"u(\d+)x(\d+)(?:s(\d+))?(?:f(\d+))?", cfg)
+        count, length, stride, first = m.groups()
+        return W.uniform_layout(int(count), int(length), int(stride) if stride else None, int(first or 0))
     return {"3a": W.cfg3_layout, "3b": lambda: W.cfg3_layout(vlog=True), "2": W.cfg2_layout,
             "4": W.cfg4_layout}[cfg]()
 
