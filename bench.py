@@ -200,6 +200,9 @@ def main():
     ap.add_argument("--no-plan-hint", action="store_true", help="pass max_len = 0 (force the planning pass)")
     ap.add_argument("--launch", default="graph", choices=["graph", "eager"],
                     help="timed steps as hipGraph replays (default; eager launches if capture fails) or eager")
+    ap.add_argument("--graph-steps", type=int, default=0,
+                    help="steps captured per hipGraph (0 = all timed steps in one graph when --steps <= 64, so the "
+                         "GPU runs them back to back; 1 = one replay per step)")
     ap.add_argument("--cpu-sample-blocks", type=int, default=4096)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU work per thread count (>= 1 pass)")
@@ -268,41 +271,62 @@ def main():
     for _ in range(args.warmup):
         step(stream)
     torch.cuda.synchronize()
-    # kernel-only time of the CRC kernel: HIP events on the launch stream, over eager steps
+    # kernel-only time of the CRC kernel, HIP events on the stream it runs on.  A step of an unsplit batch is the
+    # CRC kernel alone: under graph replay, one event pair around the timed region gives its average over the
+    # back-to-back launches.  A split batch also runs planning and combine kernels, so its CRC kernel is timed
+    # with an event pair per launch over the same number of eager steps.
+    piece = args.piece_kib * 1024 or kvsep.DEFAULT_PIECE_BYTES
+    span_timing = args.launch == "graph" and passes == 1 and 0 < max_len <= piece
     ctx.get_timing()
     ctx.set_timing(True)
-    for _ in range(args.steps if args.launch == "graph" else 0):
+    for _ in range(args.steps if args.launch == "graph" and not span_timing else 0):
         step(stream)
     torch.cuda.synchronize()
 
-    # the timed steps: one hipGraph replay per step (the step's planning kernels, memsets, CRC kernel(s) and
-    # combine captured once; kvsep_crc32c_reserve made every allocation beforehand), or eager launches
+    # the timed steps as hipGraph replays: each captured step is a full pass of the hot path (planning kernels,
+    # memsets, CRC kernel(s), combine; kvsep_crc32c_reserve made every allocation beforehand).  By default all K
+    # timed steps are captured into ONE graph, so the GPU runs them back to back instead of waiting on a host
+    # replay per step (a 50 us config-2 step otherwise pays ~7 us of replay turnaround); or eager launches.
     run = lambda: step(stream)  # noqa: E731
     launch = "eager"
+    n_calls = args.steps
     if args.launch == "graph":
         ctx.set_timing(False)  # no timing events inside the graph
+        per = args.graph_steps or (args.steps if args.steps <= 64 else 1)
+        if args.steps % per:
+            per = 1
         try:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                step(torch.cuda.current_stream())
+                for _ in range(per):
+                    step(torch.cuda.current_stream())
             g.replay()  # warm replay
             torch.cuda.synchronize()
-            run, launch = g.replay, "hipGraph"
+            run, launch, n_calls = g.replay, f"hipGraph ({per} step(s) per replay)", args.steps // per
         except Exception as e:  # keep the measurement: fall back to eager launches
             log(f"[rank {rank}] graph capture failed ({e}); timing eager launches")
             torch.cuda.synchronize()
+            span_timing = False
+            ctx.set_timing(True)
+    ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    if span_timing:
+        ev[0].record()  # the graph replays on the current stream
+    for _ in range(n_calls):
         run()
+    if span_timing:
+        ev[1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ctx.set_timing(False)
     kern_ms, launches = ctx.get_timing()
+    if span_timing:
+        kern_ms, launches = ev[0].elapsed_time(ev[1]), args.steps
     elapsed = shard.max_over_ranks(elapsed, dist if world > 1 else None, coll_dev)
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * passes * useful * args.steps / GIB / elapsed
@@ -421,6 +445,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved_gbps / HBM_PEAK_GBPS, 4), "traffic": traffic,
                          "kernel": kernel_name, "kernel_avg_ms": round(kern_avg_ms, 4),
+                         "kernel_timing": ("one HIP event pair around the timed graph replay of back-to-back "
+                                           "single-kernel steps" if span_timing else
+                                           "a HIP event pair around each launch of the CRC kernel"),
                          "algorithmic_bytes_per_launch": useful},
             "cpu_baseline": cpu,
             "read_ceiling_GBps": read_ceiling_gbps and round(read_ceiling_gbps, 1),

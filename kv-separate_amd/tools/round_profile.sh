@@ -14,7 +14,7 @@ export TMPDIR=/tmp
 cd /tmp
 B="$R/bench.py --steps 3 --warmup 1 --no-cpu --roundtrip-gib 0"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o stats --output-format csv -- python3 $R/bench.py --steps 20 --warmup 1 --no-cpu --roundtrip-gib 0 --launch eager > $O/prof.json 2> $O/prof.err || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof2 -o stats --output-format csv -- python3 $R/bench.py --config 2 --steps 20 --warmup 1 --no-cpu --roundtrip-gib 0 --launch eager > $O/prof2.json 2> $O/prof2.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof2 -o stats --output-format csv -- python3 $R/bench.py --config 2 --steps 20 --warmup 1 --no-cpu --roundtrip-gib 0 > $O/prof2.json 2> $O/prof2.err || exit 1
 for c in 3a 3b 4 2; do
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch_$c -o pmc --output-format csv -- python3 $B --config $c > $O/pmc_fetch_$c.log 2>&1 || exit 1
   timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum --kernel-trace -d $O/pmc_rdreq_$c -o pmc --output-format csv -- python3 $B --config $c > $O/pmc_rdreq_$c.log 2>&1 || exit 1
@@ -26,5 +26,5 @@ for c in 3a 3b 4 2; do
   python kv-separate_amd/tools/pmc_summary.py --config $c --fetch $O/pmc_fetch_$c --rdreq $O/pmc_rdreq_$c $L --out $O/pmc_cfg$c.json --source "rocprofv3 --pmc FETCH_SIZE / --pmc TCC_EA0_RDREQ_sum, each with --kernel-trace only, python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu --roundtrip-gib 0" > /dev/null || exit 1
 done
 python kv-separate_amd/tools/trace_summary.py $O/prof/stats_kernel_trace.csv --warmup 1 --bench $O/prof.json --out $O/kernel_trace_cfg3a.json > /dev/null || exit 1
-python kv-separate_amd/tools/trace_summary.py $O/prof2/stats_kernel_trace.csv --warmup 1 --bench $O/prof2.json --out $O/kernel_trace_cfg2.json > /dev/null || exit 1
+python kv-separate_amd/tools/trace_summary.py $O/prof2/stats_kernel_trace.csv --last 20 --bench $O/prof2.json --out $O/kernel_trace_cfg2.json > /dev/null || exit 1
 echo done

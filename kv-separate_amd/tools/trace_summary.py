@@ -21,6 +21,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--warmup", type=int, default=1, help="warm-up launches of the CRC kernel to set apart")
+    ap.add_argument("--last", type=int, default=0,
+                    help="take only the last N launches as the timed ones (graph-replay runs: warm-up steps and "
+                         "the warm replay come first)")
     ap.add_argument("--bench", default=None, help="bench.py JSON line of the same run")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
@@ -35,8 +38,9 @@ def main():
         ms = [d for _, d in v]
         e = {"calls": len(ms), "avg_ms_all": statistics.mean(ms), "min_ms": min(ms), "max_ms": max(ms)}
         if any(k in name for k in CRC_KERNELS) and len(ms) > args.warmup:
-            timed = ms[args.warmup:]
-            e.update({"warmup_ms": ms[:args.warmup], "timed_calls": len(timed),
+            cut = len(ms) - args.last if args.last and len(ms) > args.last else args.warmup
+            timed = ms[cut:]
+            e.update({"warmup_ms": ms[:cut][:8], "timed_calls": len(timed),
                       "avg_ms_timed": statistics.mean(timed), "median_ms_timed": statistics.median(timed)})
             out["crc_kernel"] = name
             out["crc_avg_ms_timed"] = e["avg_ms_timed"]
