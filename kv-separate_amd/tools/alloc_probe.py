@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--allocs", type=int, default=4)
     ap.add_argument("--passes", type=int, default=6)
+    ap.add_argument("--schedules", action="store_true", help="also time the static and round-robin schedules")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     off, ln = W.cfg3_layout()
@@ -29,17 +30,38 @@ def main():
     sink = torch.zeros(64, dtype=torch.int32, device=dev)
     ctx = kvsep.Context(0)
     ctx.reserve(off.size, total)
+    # the same kernel under the other two schedules: static contiguous runs, static round-robin pieces (all waves
+    # inside one sweeping window of the batch at any time: far fewer distinct pages in flight)
+    scheds = {"guided": ctx}
+    if args.schedules:
+        c = kvsep.Context(0)
+        c.set_schedule(False)
+        c.reserve(off.size, total)
+        scheds["static"] = c
+        os.environ["KVSEP_CRC_STATIC_RR"] = "1"
+        c = kvsep.Context(0)
+        del os.environ["KVSEP_CRC_STATIC_RR"]
+        c.set_schedule(False)
+        c.reserve(off.size, total)
+        scheds["static-rr"] = c
     for k in range(args.allocs):
         data = torch.empty(total + 64, dtype=torch.uint8, device=dev)
         kvsep.fill_splitmix64(data.data_ptr(), total, 1 + k, 0)
         torch.cuda.synchronize()
         crc, rd = [], []
+        other = {k: [] for k in scheds if k != "guided"}
         for p in range(args.passes + 1):
-            ctx.set_timing(True)
-            ctx.batch_device(data.data_ptr(), d_off, d_len, out, total_bytes=total, max_len=int(ln.max()))
-            torch.cuda.synchronize()
-            ctx.set_timing(False)
-            ms, n = ctx.get_timing()
+            for name, c in scheds.items():
+                c.set_timing(True)
+                c.batch_device(data.data_ptr(), d_off, d_len, out, total_bytes=total, max_len=int(ln.max()))
+                torch.cuda.synchronize()
+                c.set_timing(False)
+                ms, n = c.get_timing()
+                if p and name != "guided":
+                    other[name].append(total / (ms / n) / 1e6)
+                if name == "guided":
+                    gms, gn = ms, n
+            ms, n = gms, gn
             ctx.set_timing(True)
             ctx.stream_read(data.data_ptr(), total, sink)
             torch.cuda.synchronize()
@@ -50,7 +72,8 @@ def main():
                 rd.append(total / (ms2 / n2) / 1e6)
         print(f"alloc {k} @ {data.data_ptr():#x}: crc {statistics.median(crc):.0f} GB/s "
               f"(min {min(crc):.0f} max {max(crc):.0f})  read ceiling {statistics.median(rd):.0f} GB/s  "
-              f"ratio {statistics.median(crc) / statistics.median(rd):.3f}", flush=True)
+              f"ratio {statistics.median(crc) / statistics.median(rd):.3f}"
+              + "".join(f"  {k} {statistics.median(v):.0f}" for k, v in other.items()), flush=True)
         del data
         torch.cuda.empty_cache()
 
