@@ -60,11 +60,15 @@ int kvsep_crc32c_ctx_create(int device, kvsep_crc32c_ctx** out);
 void kvsep_crc32c_ctx_destroy(kvsep_crc32c_ctx* ctx);
 /* Work-item ("piece") size for splitting long blocks; default 128 KiB, min 1 KiB, multiple of 1 KiB. */
 int kvsep_crc32c_ctx_set_piece_bytes(kvsep_crc32c_ctx* ctx, uint64_t piece_bytes);
-/* 0 = static round-robin of work items over waves, 1 = guided dynamic (one atomic per run of items),
- * -1 = auto (default): guided when long blocks are split into pieces, else static. */
+/* 0 = static contiguous runs of work items per wave, 2 = static round-robin items, 1 = guided dynamic (one atomic
+ * per run of items), -1 = auto (default): guided when long blocks are split into pieces, else static. */
 int kvsep_crc32c_ctx_set_schedule(kvsep_crc32c_ctx* ctx, int dynamic);
+/* Kernel of unsplit batches: 0 = auto (default; the narrow kernel for many blocks <= 8-32 KiB), 1 = always the wide
+ * kernel, 2 = the narrow kernel whenever max_len <= 64 KiB, 3 / 4 = as 2 with 16- / 8-wave workgroups.  A choice
+ * of speed only: every kernel is exact for every block.  No environment variable changes it. */
+int kvsep_crc32c_ctx_set_kernel(kvsep_crc32c_ctx* ctx, int kernel);
 /* Pre-size scratch so later calls of up to `count` blocks / `total_bytes` bytes do not allocate
- * (required before graph capture). */
+ * (required before graph capture; covers the planned, narrow, verify and SST-verify forms). */
 int kvsep_crc32c_reserve(kvsep_crc32c_ctx* ctx, uint64_t count, uint64_t total_bytes);
 /* Kernel timing with HIP events on the caller's stream, around the main CRC kernel only. */
 int kvsep_crc32c_ctx_set_timing(kvsep_crc32c_ctx* ctx, int enable);
@@ -77,9 +81,12 @@ const char* kvsep_crc32c_kernel_name(kvsep_crc32c_ctx* ctx, uint64_t count, uint
  * out[i] = Extend(init ? init[i] : 0, base + off[i], len[i]) for i < count.
  * base/off/len/init/out are DEVICE pointers; the call is asynchronous on `stream`
  * (a hipStream_t; NULL = default stream).  Blocks may overlap and sit at any byte alignment.
- * total_bytes >= sum(len) (sizes scratch only); max_len = an upper bound on len[i] or 0 if unknown
- * (when max_len <= piece size the planning pass is skipped; a max_len that is not an upper bound gives
- * undefined results).  count <= 2^32 - 1 (else KVSEP_EINVAL). */
+ * total_bytes ~ sum(len) and max_len (an upper bound on len[i], or 0 if unknown) are performance hints:
+ * with max_len <= piece size (128 KiB) the planning pass is skipped and short blocks may run on the narrow
+ * kernel.  Results are exact whatever the hints say: a block longer than max_len is checksummed whole by
+ * the wide kernel or deferred by the narrow one, and an understated total_bytes makes the kernel fall back
+ * to one work item per block.  count <= 2^32 - 1, and <= 2^31 - 1 when the batch is planned (max_len 0 or
+ * above the piece size); else KVSEP_EINVAL. */
 int kvsep_crc32c_batch_device(kvsep_crc32c_ctx* ctx, void* stream, const void* base, const uint64_t* off,
                               const uint64_t* len, const uint32_t* init, uint32_t* out, uint64_t count,
                               uint64_t total_bytes, uint64_t max_len);
@@ -112,9 +119,11 @@ int kvsep_crc32c_batch_host_span(kvsep_crc32c_ctx* ctx, const char* host_base, u
 uint64_t kvsep_vlog_walk(const char* buf, uint64_t n, uint64_t* off, uint64_t* len, uint32_t* stored, uint64_t cap,
                          uint64_t* consumed);
 /* Recovery / GC scan: walk + one batched GPU checksum + compare.  *ngood = records before the first checksum
- * mismatch (the reader reports "checksum mismatch" there and stops), *good_bytes = end offset of the last good one. */
+ * mismatch (the reader reports "checksum mismatch" there and stops), *good_bytes = end offset of the last good one,
+ * *drop_bytes = the byte count VlogReader reports with that "checksum mismatch" (the bad record's payload length,
+ * db/value_log_reader.cc:117-120), 0 when every complete record is intact.  Any output may be null. */
 int kvsep_vlog_verify_host(kvsep_crc32c_ctx* ctx, const char* buf, uint64_t n, uint64_t* nrecords, uint64_t* ngood,
-                           uint64_t* good_bytes);
+                           uint64_t* good_bytes, uint64_t* drop_bytes);
 /* Group-commit write side: frames `count` payloads into dst (needs sum(8 + len) bytes, *written). */
 int kvsep_vlog_frame_host(kvsep_crc32c_ctx* ctx, const char* const* payload, const uint64_t* len, uint64_t count,
                           char* dst, uint64_t dst_cap, uint64_t* written);

@@ -1,10 +1,10 @@
-// kvsep_leveldb_crc32c.h -- source-compatible stand-in for the reference's util/crc32c.h
-// (/root/reference/util/crc32c.h:11-41): same namespace, same signatures, same inline helpers,
-// with Extend forwarded to libkvsep_crc32c (include/kvsep_crc32c.h).  A LevelDB/KVDB build that
-// includes this instead of util/crc32c.h and drops util/crc32c.cc from its sources links against
-// -lkvsep_crc32c and needs no other change at its call sites (db/value_log_writer.cc:57,
-// db/value_log_reader.cc:110, db/log_writer.cc:19,98, db/log_reader.cc:248,
-// table/table_builder.cc:223-224, table/format.cc:102).
+// kvsep_leveldb_crc32c.h -- stand-in for the reference's util/crc32c.h (util/crc32c.h:11-41): same
+// namespace, same declarations, same inline helpers.  Extend is declared, not defined, exactly as in
+// util/crc32c.h:17: libkvsep_crc32c.so exports the out-of-line definition (csrc/leveldb_abi.cpp), so a
+// KVDB build can either keep its own util/crc32c.h or include this one -- both resolve
+// leveldb::crc32c::Extend to the library at link time once util/crc32c.cc is dropped from the sources.
+// Call sites: db/value_log_writer.cc:57, db/value_log_reader.cc:110, db/log_writer.cc:19,98,
+// db/log_reader.cc:248, table/table_builder.cc:223-224, table/format.cc:102.
 #ifndef KVSEP_LEVELDB_CRC32C_H_
 #define KVSEP_LEVELDB_CRC32C_H_
 
@@ -16,10 +16,9 @@
 namespace leveldb {
 namespace crc32c {
 
-// util/crc32c.h:17 -- crc32c of concat(A, data[0,n-1]) where init_crc = crc32c(A).
-inline uint32_t Extend(uint32_t init_crc, const char* data, size_t n) {
-  return kvsep_crc32c_extend(init_crc, data, n);
-}
+// util/crc32c.h:17 -- crc32c of concat(A, data[0,n-1]) where init_crc = crc32c(A).  Defined in
+// libkvsep_crc32c.so (C++ linkage, = kvsep_crc32c_extend).
+uint32_t Extend(uint32_t init_crc, const char* data, size_t n);
 
 // util/crc32c.h:20
 inline uint32_t Value(const char* data, size_t n) { return Extend(0, data, n); }

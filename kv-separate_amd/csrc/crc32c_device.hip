@@ -57,8 +57,9 @@ struct DevTables {
   uint32_t zpiece[4][256];  // Z_piece_bytes, used by the combine kernel
   uint32_t znarrow[4][256]; // Z_{16 kNarrowLanes}: the replicated table of the narrow kernel
   uint32_t zsmall[3][4][256];  // Z_16K, Z_32K, Z_64K: the automatic smaller pieces of small batches
+  uint32_t x2n[64];         // x^(2^k) mod P (reflected): Z_n for ANY n by square-and-multiply (gf2_shift)
 };
-static_assert(sizeof(DevTables) == 4096 * 13 + 1024, "table layout");
+static_assert(sizeof(DevTables) == 4096 * 13 + 1024 + 256, "table layout");
 constexpr uint64_t kSmallPiece = 16 * 1024;  // zsmall[k] is Z_{kSmallPiece << k}
 
 struct PiecesArgs {
@@ -71,7 +72,8 @@ struct PiecesArgs {
   unsigned long long* first_bad;
   unsigned long long* nbad;
   uint64_t count;
-  const uint32_t* pstart;           // planned mode: piece range of block b = [pstart[b], pstart[b+1])
+  const uint64_t* pstart;           // planned mode: piece range of block b = [pstart[b], pstart[b+1]) (u64: an
+                                    // understated total_bytes cannot wrap the scan, see the max_pieces fallback)
   const uint32_t* pblk;             // planned mode: block of piece g
   uint32_t* partial;                // planned mode: raw register of piece g
   uint32_t* work_counter;           // dynamic schedule
@@ -79,6 +81,7 @@ struct PiecesArgs {
   const uint32_t* zpiece;           // Z_piece_bytes as 4 byte tables (combine kernel)
   uint64_t max_pieces;              // capacity of pblk/partial
   uint32_t static_contig;           // static schedule: contiguous item ranges per wave (else round-robin)
+  uint64_t hint;                    // narrow kernel: the caller's max_len hint; longer blocks are deferred (exact)
   const DevTables* tabs;
 };
 
@@ -345,6 +348,27 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
 
 __device__ __forceinline__ uint32_t mask_crc(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xa282ead8u; }
 
+// a * b mod P in the reflected representation (bit 31 = x^0): carry-less multiply by VALU shifts, no tables.
+__device__ __forceinline__ uint32_t gf2_mulmod(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+#pragma unroll 8
+  for (int i = 31; i >= 0; --i) {
+    p ^= (0u - ((a >> i) & 1u)) & b;
+    b = (b >> 1) ^ (0x82F63B78u & (0u - (b & 1u)));
+  }
+  return p;
+}
+
+// Z_n(reg): the register advanced over n zero bytes, for any n, = reg * x^(8n) mod P (x2n[k] = x^(2^k) mod P).
+// A few thousand VALU operations: only for the rare paths that need an arbitrary shift (gf2.h has the host side).
+__device__ uint32_t gf2_shift(const DevTables* tabs, uint32_t reg, uint64_t n) {
+  const uint64_t e = n << 3;
+  uint32_t p = 0x80000000u;  // x^0
+  for (int k = 0; k < 64; ++k)
+    if ((e >> k) & 1u) p = gf2_mulmod(tabs->x2n[k], p);
+  return gf2_mulmod(p, reg);
+}
+
 __device__ __forceinline__ void emit_block(const PiecesArgs& a, uint64_t b, uint32_t crc) {
   a.out[b] = crc;
   if (a.expect && mask_crc(crc) != a.expect[b]) {
@@ -478,7 +502,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
       bool first, only;
       if (planned) {
         b = a.pblk[g];
-        const uint64_t s0 = a.pstart[b], k = uint64_t(a.pstart[b + 1]) - s0, j = g - s0;
+        const uint64_t s0 = a.pstart[b], k = a.pstart[b + 1] - s0, j = g - s0;
         const uint64_t n = a.len[b];
         re = n - (k - 1 - j) * a.piece_bytes;
         rs = j ? n - (k - j) * a.piece_bytes : 0;
@@ -735,27 +759,39 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   // array, shared by the slot's 8 lanes), so no descriptor load sits between two groups' row loads.
   // The raw loaded words are kept and only used at the take, a group later: nothing consumes them right
   // after the loads, so the compiler's wait for them lands at the take, not behind the loads.
-  struct Desc {  // 32-bit length: the narrow kernel runs only under a max_len hint <= 64 KiB (a 64-bit end
-    uint64_t off;  // spills at 16 waves)
-    uint32_t len, init;
+  // The kernel is chosen on the caller's max_len hint (<= 32 KiB), but a hint is never trusted for exactness: a
+  // block longer than the hint (a.hint) is left out of its group and redone by its wave at the end of the run
+  // (`deferred`), with its full 64-bit length.  The staged length stays 32-bit: a 64-bit block end spills at 16
+  // waves.
+  struct Desc {
+    uint64_t off;
+    uint32_t len, lenhi, init;
   };
   auto load_desc = [&](uint64_t g, Desc& d) {  // block g + slot; past hi: loads stay in bounds, take() empties it
     const uint64_t b = g + slot;
     const uint64_t bb = b < hi ? b : hi - 1;
     d.off = a.off[bb];
-    d.len = reinterpret_cast<const uint32_t*>(a.len + bb)[0];  // low word (LE) only: a dead high word's
-                                                               // register got reused, forcing an early wait
+    const uint2 l = *reinterpret_cast<const uint2*>(a.len + bb);  // one 8-B load, both words consumed at the take
+    d.len = l.x;
+    d.lenhi = l.y;
     d.init = *(a.init ? a.init + bb : &a.tabs->z4[0][0]);  // no init: a word that is 0 (Z_4 of byte 0)
   };
   struct NItem {  // the slot's block is g + slot (g: the group's first block, wave-uniform)
     uint32_t reg0;
     uint32_t kmin, kmax;
+    bool over;  // this lane's block exceeds the hint: skipped here, redone at the end of the run
   };
   Desc dn;  // descriptors of the next group to take
+  bool deferred = false;  // wave-uniform: some block of this wave's run exceeded the hint
+  const uint32_t hint32 = uint32_t(a.hint);  // <= 64 KiB (use_narrow)
   auto take = [&](uint64_t g, NItem& it, NStaged<kG>& st) {
-    const bool live = g + slot < hi;
+    const bool in = g + slot < hi;
+    const bool over = in && (dn.lenhi != 0 || dn.len > hint32);
+    deferred |= __builtin_amdgcn_ballot_w64(over) != 0;
+    const bool live = in && !over;
     const uintptr_t ps = live ? reinterpret_cast<uintptr_t>(a.base) + dn.off : dummy;
     it.reg0 = ~dn.init;
+    it.over = over;
     nstage<kG, kNT>(st, ps, ps + (live ? dn.len : 0u), j, dummy);
     uint32_t km = 0, kn = ~0u;
 #pragma unroll
@@ -773,7 +809,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     // end it is an empty group of dummy loads: see the wide kernel's step())
     const uint32_t reg = nfinish<kG, kNT>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
                                           [&]() { take(gn, ib, B); });
-    if (j == kNarrowLanes - 1 && g + slot < hi) emit_block(a, g + slot, ~reg);
+    if (j == kNarrowLanes - 1 && g + slot < hi && !ia.over) emit_block(a, g + slot, ~reg);
     load_desc(gn + kPerGroup, dn);  // here, where this group's registers are dead
     return gn < hi;
   };
@@ -807,6 +843,45 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
       if (!step(g + kPerGroup, nxt, T, cur, S)) break;
     }
   }
+  if (deferred) {
+    // Blocks longer than the hint: the wave walks its run again and checksums those blocks one at a time, each
+    // cut into 8 contiguous sub-ranges, one per slot (full 64-bit length), merged with R(A||B) = Z_|B|(R(A)) ^ R(B)
+    // through gf2_shift.  Slower than the main path (long blocks are not what this kernel is for) but exact.
+    for (uint64_t g = lo; g < hi; g += kPerGroup) {
+      Desc d;
+      load_desc(g, d);
+      uint64_t over = __builtin_amdgcn_ballot_w64(g + slot < hi && (d.lenhi != 0 || d.len > hint32));
+      while (over) {
+        const uint32_t k = uint32_t(__builtin_ctzll(over)) / kNarrowLanes;  // slot of the next deferred block
+        over &= ~(0xffull << (k * kNarrowLanes));
+        const uint32_t src = k * kNarrowLanes;
+        const uint64_t boff = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(d.off >> 32)), int(src)))) << 32) |
+                              uint32_t(__builtin_amdgcn_readlane(int(uint32_t(d.off)), int(src)));
+        const uint64_t L = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(d.lenhi), int(src)))) << 32) |
+                           uint32_t(__builtin_amdgcn_readlane(int(d.len), int(src)));
+        const uint32_t binit = uint32_t(__builtin_amdgcn_readlane(int(d.init), int(src)));
+        const uint64_t q = L / kPerGroup;
+        const uint64_t rs = uint64_t(slot) * q, re = slot == kPerGroup - 1 ? L : rs + q;
+        const uintptr_t blk = reinterpret_cast<uintptr_t>(a.base) + boff;
+        NStaged<kG> X;
+        nstage<kG, kNT>(X, blk + rs, blk + re, j, dummy);
+        uint32_t km = 0, kn = ~0u;
+#pragma unroll
+        for (uint32_t t = 0; t < kPerGroup; ++t) {
+          const uint32_t kk = uint32_t(__builtin_amdgcn_readlane(int(X.K), int(t * kNarrowLanes)));
+          km = km > kk ? km : kk;
+          kn = kn < kk ? kn : kk;
+        }
+        uint32_t reg = nfinish<kG, kNT>(lds, X, slot == 0 ? ~binit : 0u, j, lc0, lc1, kn, km, dummy, NoMid());
+        if (j == kNarrowLanes - 1) reg = gf2_shift(a.tabs, reg, L - re);  // carried to the block's end
+        uint32_t acc = 0;
+#pragma unroll
+        for (uint32_t t = 0; t < kPerGroup; ++t)
+          acc ^= uint32_t(__builtin_amdgcn_readlane(int(reg), int(t * kNarrowLanes + kNarrowLanes - 1)));
+        if (lane == 0) emit_block(a, g + k, ~acc);
+      }
+    }
+  }
 }
 
 // One thread per block: Horner over the block's pieces, R <- Z_piece(R) ^ R_piece.
@@ -816,10 +891,10 @@ __global__ void __launch_bounds__(256) crc32c_combine_kernel(PiecesArgs a) {
   __syncthreads();
   const uint64_t b = uint64_t(blockIdx.x) * 256 + threadIdx.x;
   if (b >= a.count) return;
-  const uint32_t s = a.pstart[b], e = a.pstart[b + 1];
+  const uint64_t s = a.pstart[b], e = a.pstart[b + 1];
   if (e - s <= 1 || a.pstart[a.count] > a.max_pieces) return;  // unsplit fallback: already emitted
   uint32_t acc = a.partial[s];
-  for (uint32_t g = s + 1; g < e; ++g) {
+  for (uint64_t g = s + 1; g < e; ++g) {
     acc = zp[acc & 255u] ^ zp[256 + ((acc >> 8) & 255u)] ^ zp[512 + ((acc >> 16) & 255u)] ^ zp[768 + (acc >> 24)];
     acc ^= a.partial[g];
   }
@@ -827,14 +902,14 @@ __global__ void __launch_bounds__(256) crc32c_combine_kernel(PiecesArgs a) {
 }
 
 __global__ void crc32c_plan_count_kernel(const uint64_t* len, uint64_t count, uint64_t piece_bytes,
-                                         uint32_t* counts) {
+                                         uint64_t* counts) {
   const uint64_t b = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (b >= count) return;
   const uint64_t n = len[b];
   // floor, not ceil: piece 0 takes the remainder ON TOP of a full piece (length in [P, 2P)), so no block ends
   // up with a short remainder piece that costs a work item of its own (3b: 33-B pieces, one per record);
   // only the later pieces must be exactly P long for the combine's Z_P.
-  counts[b] = n < 2 * piece_bytes ? 1u : uint32_t(n / piece_bytes);
+  counts[b] = n < 2 * piece_bytes ? 1u : n / piece_bytes;
 }
 
 // SST write side (table/table_builder.cc:222-225): crc = Extend(Value(block), &type, 1); trailer word = Mask(crc).
@@ -858,12 +933,12 @@ __global__ void sst_verify_prep_kernel(const uint8_t* base, const uint64_t* off,
   stored[i] = uint32_t(t[0]) | (uint32_t(t[1]) << 8) | (uint32_t(t[2]) << 16) | (uint32_t(t[3]) << 24);
 }
 
-__global__ void crc32c_plan_expand_kernel(const uint32_t* pstart, uint64_t count, uint64_t max_pieces,
+__global__ void crc32c_plan_expand_kernel(const uint64_t* pstart, uint64_t count, uint64_t max_pieces,
                                           uint32_t* pblk) {
   const uint64_t b = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (b >= count) return;
-  const uint32_t s = pstart[b], e = pstart[b + 1];
-  for (uint32_t g = s; g < e && g < max_pieces; ++g) pblk[g] = uint32_t(b);
+  const uint64_t s = pstart[b], e = pstart[b + 1];
+  for (uint64_t g = s; g < e && g < max_pieces; ++g) pblk[g] = uint32_t(b);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -933,9 +1008,10 @@ struct kvsep_crc32c_ctx {
   uint64_t piece_bytes = 128 * 1024;  // best of 32 KiB .. 1 MiB on configs 3a/3b/4
   bool piece_auto = true;             // smaller pieces for small batches (piece_for); off once set explicitly
   int dynamic = -1;  // -1 auto, 0 static, 1 guided
-  int variant = 1;   // rows per prefetch group / load policy, see launch_pieces
-  uint32_t static_contig = 1;
-  int narrow = 1;    // route batches of short blocks to the narrow kernel (use_narrow; 0 = never)
+  int kernel = 0;    // kvsep_crc32c_ctx_set_kernel: 0 auto (use_narrow), 1 wide only, 2-4 narrow when the hint allows
+  uint32_t static_contig = 1;  // static schedule: contiguous runs (1) or round-robin items (0, set_schedule(2))
+  int variant = 1;   // KVSEP_DIAG builds only: A/B and ablation variants of the wide kernel (launch_pieces_v)
+  int narrow = 1;    // KVSEP_DIAG builds only: narrow-kernel variants
   Scratch sc;  // scratch of the calls made directly on this context (any stream, event-ordered)
   // timing
   bool timing = false;
@@ -974,6 +1050,7 @@ int upload_tables(kvsep_crc32c_ctx* c) {
   gf2::byte_tables(gf2::zero_bytes_map(c->piece_bytes), &h.zpiece[0][0]);
   for (int k = 0; k < 3; ++k) gf2::byte_tables(gf2::zero_bytes_map(kSmallPiece << k), &h.zsmall[k][0][0]);
   gf2::byte_tables(gf2::zero_bytes_map(kNarrowRow), &h.znarrow[0][0]);
+  gf2::x2n_table(h.x2n);
   if (!c->d_tabs) KVSEP_HIP(hipMalloc(&c->d_tabs, sizeof(DevTables)));
   KVSEP_HIP(hipMemcpy(c->d_tabs, &h, sizeof(DevTables), hipMemcpyHostToDevice));
   return KVSEP_OK;
@@ -982,7 +1059,8 @@ int upload_tables(kvsep_crc32c_ctx* c) {
 void free_plan(Scratch& sc) {
   hipFree(sc.d_counts); hipFree(sc.d_pstart); hipFree(sc.d_pblk); hipFree(sc.d_partial);
   hipFree(sc.d_scan_tmp);
-  sc.d_counts = sc.d_pstart = sc.d_pblk = sc.d_partial = nullptr;
+  sc.d_counts = sc.d_pstart = nullptr;
+  sc.d_pblk = sc.d_partial = nullptr;
   sc.d_scan_tmp = nullptr;
   sc.cap_count = sc.cap_pieces = 0;
   sc.scan_tmp_bytes = 0;
@@ -1008,16 +1086,34 @@ int release(Scratch& sc, hipStream_t s) {
   return KVSEP_OK;
 }
 
+// SST verify scratch (len + 1 and the stored trailer words per block).
+int ensure_sst(Scratch& sc, uint64_t count) {
+  if (count <= sc.cap_sst) return KVSEP_OK;
+  int rc = quiesce(sc);
+  if (rc) return rc;
+  hipFree(sc.d_sst_len1);
+  hipFree(sc.d_sst_stored);
+  sc.d_sst_len1 = nullptr;
+  sc.d_sst_stored = nullptr;
+  sc.cap_sst = 0;
+  KVSEP_HIP(hipMalloc(&sc.d_sst_len1, count * 8));
+  KVSEP_HIP(hipMalloc(&sc.d_sst_stored, count * 4));
+  sc.cap_sst = count;
+  return KVSEP_OK;
+}
+
 int ensure_plan(Scratch& sc, uint64_t piece_bytes, uint64_t count, uint64_t total_bytes) {
   const uint64_t pieces = count + total_bytes / piece_bytes + 1;
-  if (count > 0xffffffffull || pieces > 0xffffffffull) return set_err(KVSEP_EINVAL, "batch too large for u32 piece indices");
+  // hipcub's scan takes an int item count; piece and block indices are u32 in the kernels
+  if (count > 0x7fffffffull) return set_err(KVSEP_EINVAL, "more than 2^31 - 1 blocks in one batch that needs a plan");
+  if (pieces > 0xffffffffull) return set_err(KVSEP_EINVAL, "batch too large for u32 piece indices");
   if (count <= sc.cap_count && pieces <= sc.cap_pieces) return KVSEP_OK;
   const uint64_t nc = std::max<uint64_t>(count, sc.cap_count), np = std::max<uint64_t>(pieces, sc.cap_pieces);
   int rc = quiesce(sc);
   if (rc) return rc;
   free_plan(sc);
-  KVSEP_HIP(hipMalloc(&sc.d_counts, nc * 4));
-  KVSEP_HIP(hipMalloc(&sc.d_pstart, (nc + 1) * 4));
+  KVSEP_HIP(hipMalloc(&sc.d_counts, nc * 8));
+  KVSEP_HIP(hipMalloc(&sc.d_pstart, (nc + 1) * 8));
   KVSEP_HIP(hipMalloc(&sc.d_pblk, np * 4));
   KVSEP_HIP(hipMalloc(&sc.d_partial, np * 4));
   size_t tb = 0;
@@ -1036,11 +1132,16 @@ int ensure_plan(Scratch& sc, uint64_t piece_bytes, uint64_t count, uint64_t tota
 //   <= 16 KiB blocks from 16 Ki blocks up (16 Ki x 16 KiB: 5.58 vs 5.36; 4 Ki x 16 KiB: wide 3.67 vs 2.58),
 //   <= 32 KiB blocks from 32 Ki blocks up (32 Ki x 32 KiB: 6.72 vs 6.35; 16 Ki x 32 KiB: wide 6.12 vs 6.06),
 //   64 KiB blocks never (16 Ki x 64 KiB: wide 6.22 vs 4.88).
-// The thresholds scale with the CU count (256 on MI355X).
-// KVSEP_NARROW: 0 never, 1 this rule (default), 2..7, 9 always when max_len <= 64 KiB (tests, A/B).
+// The thresholds scale with the CU count (256 on MI355X).  kvsep_crc32c_ctx_set_kernel can force either kernel
+// (tests); the choice never changes a result: both are exact for any block, whatever the hint.
 bool use_narrow(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t max_len) {
-  if (!c->narrow || max_len == 0) return false;
-  if (c->narrow >= 2) return max_len <= 2 * kNarrowMax;
+  if (max_len == 0 || max_len > 2 * kNarrowMax) return false;
+  if (c->kernel == 1) return false;
+  if (c->kernel >= 2) return true;
+#ifdef KVSEP_DIAG
+  if (!c->narrow) return false;
+  if (c->narrow >= 2) return true;
+#endif
   const uint64_t cus = uint64_t(c->num_cus);
   return (max_len <= 8 * 1024 && count >= 32 * cus) || (max_len <= 16 * 1024 && count >= 64 * cus) ||
          (max_len <= kNarrowMax && count >= 128 * cus);
@@ -1082,16 +1183,20 @@ void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs
   // both tried and measured slower: -2 to -7 % and -2 to -4 %; the extra VGPRs cost LDS-lookup overlap)
   //   5: 16-wave workgroups (the round-1 kernel)    6: 12-wave workgroups    7: 4-wave workgroups, 8-row groups
   //   8, 9: diagnostic ablations (wrong results)
+  // Only the default is compiled into the shipped library; the rest exist in the KVSEP_DIAG tools build
+  // (`make -C kv-separate_amd diag` -> tools/libkvsep_diag.so), and 8 and 9 give wrong results by design.
   constexpr int T = kWgThreads;
   switch (variant) {
+#ifdef KVSEP_DIAG
     case 0: crc32c_pieces_kernel<P, D, 4, false, true, 0, T><<<grid, T, 0, s>>>(a); break;
     case 2: crc32c_pieces_kernel<P, D, 4, true, false, 0, T><<<grid, T, 0, s>>>(a); break;
     case 3: crc32c_pieces_kernel<P, D, 8, true, true, 0, T><<<grid, T, 0, s>>>(a); break;
     case 5: crc32c_pieces_kernel<P, D, 4, true, true, 0, 1024><<<grid, 1024, 0, s>>>(a); break;
     case 6: crc32c_pieces_kernel<P, D, 4, true, true, 0, 768><<<grid, 768, 0, s>>>(a); break;
     case 7: crc32c_pieces_kernel<P, D, 8, true, true, 0, 256><<<grid, 256, 0, s>>>(a); break;
-    case 8: crc32c_pieces_kernel<P, D, 4, true, true, 1, T><<<grid, T, 0, s>>>(a); break;  // diag
-    case 9: crc32c_pieces_kernel<P, D, 4, true, true, 2, T><<<grid, T, 0, s>>>(a); break;  // diag
+    case 8: crc32c_pieces_kernel<P, D, 4, true, true, 1, T><<<grid, T, 0, s>>>(a); break;  // ablation
+    case 9: crc32c_pieces_kernel<P, D, 4, true, true, 2, T><<<grid, T, 0, s>>>(a); break;  // ablation
+#endif
     default: crc32c_pieces_kernel<P, D, 4, true, true, 0, T><<<grid, T, 0, s>>>(a); break;
   }
 }
@@ -1117,7 +1222,8 @@ int launch_batch(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* ba
   if (!base || !off || !len || !out) return set_err(KVSEP_EINVAL, "null pointer argument");
   // block indices travel as u32 through the descriptor windows and the piece table
   if (count > 0xffffffffull) return set_err(KVSEP_EINVAL, "more than 2^32 - 1 blocks in one batch");
-  KVSEP_HIP(hipSetDevice(c->device));
+  DeviceGuard dg(c->device);
+  KVSEP_HIP(dg.err);
   // Under stream capture (hipGraph) the call only records its nodes: the cross-stream scratch events are
   // skipped (a captured wait on an event recorded outside the capture is not allowed), so the graph's user
   // orders its replays against other uses of this context's scratch.  Allocation must not happen either:
@@ -1168,7 +1274,7 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     const unsigned nb = unsigned((count + 255) / 256);
     crc32c_plan_count_kernel<<<nb, 256, 0, s>>>(len, count, a.piece_bytes, sc.d_counts);
     KVSEP_HIP(hipGetLastError());
-    KVSEP_HIP(hipMemsetAsync(sc.d_pstart, 0, 4, s));
+    KVSEP_HIP(hipMemsetAsync(sc.d_pstart, 0, 8, s));
     size_t tb = sc.scan_tmp_bytes;
     KVSEP_HIP(hipcub::DeviceScan::InclusiveSum(sc.d_scan_tmp, tb, sc.d_counts, sc.d_pstart + 1, int(count), s));
     crc32c_plan_expand_kernel<<<nb, 256, 0, s>>>(sc.d_pstart, count, sc.cap_pieces, sc.d_pblk);
@@ -1203,12 +1309,18 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     // LDS fill with the first group's loads (9; +0.3-2 % over 2); at 16 waves that overlap measured -5 %.
     // 2: always 8 waves; 3: 12 waves; 4 / 5: 8-row groups at 8 / 12 waves; 6: always 16 waves; 7: as 1; 9: 8 waves, fill overlapped with the first loads.
     const bool eight_waves = max_len <= 8 * 1024 ? count >= (1u << 17) : count >= (1u << 15);
-    const int nv = (c->narrow == 1 || c->narrow == 7) ? (eight_waves ? 9 : 6) : c->narrow;
+    int nv = c->kernel == 3 ? 6 : c->kernel == 4 ? 9 : (eight_waves ? 9 : 6);
+#ifdef KVSEP_DIAG
+    if (c->narrow != 1 && c->narrow != 7 && c->kernel < 3) nv = c->narrow;
+#endif
+    a.hint = max_len;
     switch (nv) {
+#ifdef KVSEP_DIAG
       case 2: crc32c_narrow_kernel<4, true, 512><<<grid, 512, 0, s>>>(a); break;
       case 3: crc32c_narrow_kernel<4, true, 768><<<grid, 768, 0, s>>>(a); break;
       case 4: crc32c_narrow_kernel<8, true, 512><<<grid, 512, 0, s>>>(a); break;
       case 5: crc32c_narrow_kernel<8, true, 768><<<grid, 768, 0, s>>>(a); break;
+#endif
       case 9: crc32c_narrow_kernel<4, true, 512, true><<<grid, 512, 0, s>>>(a); break;
       default: crc32c_narrow_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
     }
@@ -1272,13 +1384,16 @@ int kvsep_crc32c_ctx_create(int device, kvsep_crc32c_ctx** out) {
     std::string m = std::string("device is ") + prop.gcnArchName + ", this build targets gfx950 only";
     return set_err(KVSEP_ENODEV, m.c_str());
   }
+  DeviceGuard dg(device);
+  KVSEP_HIP(dg.err);
   auto* c = new kvsep_crc32c_ctx();
   c->device = device;
   c->num_cus = prop.multiProcessorCount;
+#ifdef KVSEP_DIAG  // tools build only: no environment variable reaches the shipped library's kernel choice
   if (const char* v = std::getenv("KVSEP_CRC_VARIANT")) c->variant = std::atoi(v);
   if (const char* v = std::getenv("KVSEP_NARROW")) c->narrow = std::atoi(v);
   if (const char* v = std::getenv("KVSEP_CRC_STATIC_RR")) c->static_contig = std::atoi(v) ? 0 : 1;
-  KVSEP_HIP(hipSetDevice(device));
+#endif
   int rc = upload_tables(c);
   if (rc) {
     delete c;
@@ -1290,7 +1405,7 @@ int kvsep_crc32c_ctx_create(int device, kvsep_crc32c_ctx** out) {
 
 void kvsep_crc32c_ctx_destroy(kvsep_crc32c_ctx* c) {
   if (!c) return;
-  hipSetDevice(c->device);
+  DeviceGuard dg(c->device);
   hipDeviceSynchronize();
   free_scratch(c->sc);
   hipFree(c->d_tabs);
@@ -1303,7 +1418,8 @@ void kvsep_crc32c_ctx_destroy(kvsep_crc32c_ctx* c) {
 int kvsep_crc32c_ctx_set_piece_bytes(kvsep_crc32c_ctx* c, uint64_t piece_bytes) {
   if (!c || piece_bytes < 1024 || piece_bytes % 1024) return set_err(KVSEP_EINVAL, "piece_bytes must be a multiple of 1 KiB");
   std::lock_guard<std::mutex> g(c->mu);
-  KVSEP_HIP(hipSetDevice(c->device));
+  DeviceGuard dg(c->device);
+  KVSEP_HIP(dg.err);
   KVSEP_HIP(hipDeviceSynchronize());
   c->piece_bytes = piece_bytes;
   c->piece_auto = false;
@@ -1314,18 +1430,30 @@ int kvsep_crc32c_ctx_set_piece_bytes(kvsep_crc32c_ctx* c, uint64_t piece_bytes) 
 
 int kvsep_crc32c_ctx_set_schedule(kvsep_crc32c_ctx* c, int dynamic) {
   if (!c) return set_err(KVSEP_EINVAL, "null ctx");
-  c->dynamic = dynamic < 0 ? -1 : (dynamic ? 1 : 0);
+  std::lock_guard<std::mutex> g(c->mu);
+  c->dynamic = dynamic < 0 ? -1 : (dynamic == 1 ? 1 : 0);
+  c->static_contig = dynamic == 2 ? 0 : 1;
+  return KVSEP_OK;
+}
+
+int kvsep_crc32c_ctx_set_kernel(kvsep_crc32c_ctx* c, int kernel) {
+  if (!c || kernel < 0 || kernel > 4) return set_err(KVSEP_EINVAL, "kernel must be 0..4");
+  std::lock_guard<std::mutex> g(c->mu);
+  c->kernel = kernel;
   return KVSEP_OK;
 }
 
 int kvsep_crc32c_reserve(kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes) {
   if (!c) return set_err(KVSEP_EINVAL, "null ctx");
   std::lock_guard<std::mutex> g(c->mu);
-  KVSEP_HIP(hipSetDevice(c->device));
+  DeviceGuard dg(c->device);
+  KVSEP_HIP(dg.err);
   // everything a later call could allocate, so that the call can be captured into a hipGraph
   if (!c->sc.d_counter) KVSEP_HIP(hipMalloc(&c->sc.d_counter, 16));
   if (!c->sc.d_verify) KVSEP_HIP(hipMalloc(&c->sc.d_verify, 16));
   if (!c->sc.last_use) KVSEP_HIP(hipEventCreateWithFlags(&c->sc.last_use, hipEventDisableTiming));
+  int rc = ensure_sst(c->sc, count);
+  if (rc) return rc;
   const uint32_t* zp = nullptr;
   return ensure_plan(c->sc, piece_for(c, total_bytes, &zp), count, total_bytes);
 }
@@ -1415,22 +1543,19 @@ int kvsep_sst_verify_device(kvsep_crc32c_ctx* c, void* stream, const void* file_
   if (!c || !file_base || !off || !len || !out) return set_err(KVSEP_EINVAL, "null argument");
   std::lock_guard<std::mutex> g(c->mu);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  KVSEP_HIP(hipSetDevice(c->device));
+  DeviceGuard dg(c->device);
+  KVSEP_HIP(dg.err);
   Scratch& sc = c->sc;
-  int rc = acquire(sc, s);
+  // as launch_batch: under capture no cross-stream events and no allocation (kvsep_crc32c_reserve sizes SST
+  // scratch too)
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  KVSEP_HIP(hipStreamIsCapturing(s, &cap));
+  const bool capturing = cap != hipStreamCaptureStatusNone;
+  if (capturing && count > sc.cap_sst) return set_err(KVSEP_EINVAL, "SST verify under capture needs kvsep_crc32c_reserve first");
+  int rc = capturing ? KVSEP_OK : acquire(sc, s);
   if (rc) return rc;
-  if (count > sc.cap_sst) {
-    rc = quiesce(sc);
-    if (rc) return rc;
-    hipFree(sc.d_sst_len1);
-    hipFree(sc.d_sst_stored);
-    sc.d_sst_len1 = nullptr;
-    sc.d_sst_stored = nullptr;
-    sc.cap_sst = 0;
-    KVSEP_HIP(hipMalloc(&sc.d_sst_len1, count * 8));
-    KVSEP_HIP(hipMalloc(&sc.d_sst_stored, count * 4));
-    sc.cap_sst = count;
-  }
+  rc = ensure_sst(sc, count);
+  if (rc) return rc;
   if (count) {
     sst_verify_prep_kernel<<<unsigned((count + 255) / 256), 256, 0, s>>>(static_cast<const uint8_t*>(file_base), off,
                                                                         len, sc.d_sst_len1, sc.d_sst_stored, count);
@@ -1439,7 +1564,7 @@ int kvsep_sst_verify_device(kvsep_crc32c_ctx* c, void* stream, const void* file_
   rc = launch_batch_in(c, sc, s, file_base, off, sc.d_sst_len1, nullptr, sc.d_sst_stored, out, first_bad, nbad, count,
                        total_bytes + count, max_len ? max_len + 1 : 0);
   if (rc) return rc;
-  return release(sc, s);
+  return capturing ? KVSEP_OK : release(sc, s);
 }
 
 const char* kvsep_crc32c_kernel_name(kvsep_crc32c_ctx* c, uint64_t count, uint64_t max_len) {
@@ -1454,6 +1579,8 @@ int kvsep_stream_read_device(kvsep_crc32c_ctx* c, void* stream, const void* src,
   const uint64_t n16 = nbytes / 16;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   std::lock_guard<std::mutex> g(c->mu);
+  DeviceGuard dg(c->device);
+  KVSEP_HIP(dg.err);
   if (c->timing) {
     e0 = take_event(c);
     e1 = take_event(c);

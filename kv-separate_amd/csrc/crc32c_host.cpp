@@ -213,10 +213,7 @@ int hip_fail(const char* what, hipError_t e) {
     if (_e != hipSuccess) return hip_fail(#call, _e); \
   } while (0)
 
-int ensure_staging(kvsep_crc32c_ctx* c) {
-  HostStaging& s = ctx_staging(c);
-  if (s.ready) return KVSEP_OK;
-  KVSEP_HIPH(hipSetDevice(ctx_device(c)));
+int ensure_staging_once(HostStaging& s) {
   s.bytes = kSlotBytes;
   s.max_blocks = kSlotBlocks;
   for (int i = 0; i < HostStaging::kSlots; ++i) {
@@ -230,6 +227,29 @@ int ensure_staging(kvsep_crc32c_ctx* c) {
     KVSEP_HIPH(hipMalloc(&s.d_out[i], s.max_blocks * 4));
     KVSEP_HIPH(hipStreamCreateWithFlags(&s.stream[i], hipStreamNonBlocking));
     KVSEP_HIPH(hipEventCreateWithFlags(&s.done[i], hipEventDisableTiming));
+  }
+  return KVSEP_OK;
+}
+
+// Pinned slots, device slots, streams and events of the host entry points, created on first use.  A failure
+// part-way frees what was created (nothing leaks into the next attempt) and is remembered, so the framing
+// writers' payload copies go straight to memcpy instead of retrying the allocation on every call.
+int ensure_staging(kvsep_crc32c_ctx* c) {
+  HostStaging& s = ctx_staging(c);
+  if (s.ready) return KVSEP_OK;
+  if (s.failed) {
+    set_last_error("host staging could not be allocated earlier on this context");
+    return KVSEP_ENOMEM;
+  }
+  DeviceGuard dg(ctx_device(c));
+  if (dg.err != hipSuccess) return hip_fail("hipSetDevice", dg.err);
+  const int rc = ensure_staging_once(s);
+  if (rc != KVSEP_OK) {
+    std::string msg = kvsep_last_error();
+    release_staging(s);
+    s.failed = true;
+    set_last_error(msg.c_str());
+    return rc;
   }
   s.pool = copy_pool_create();
   s.ready = true;
@@ -320,16 +340,25 @@ int big_block(kvsep_crc32c_ctx* c, HostStaging& s, SlotJob* jobs, uint32_t* out,
   return KVSEP_OK;
 }
 
+// The drop-in's context: one per device, on the CALLER's current device (a rank bound to GPU N checksums on
+// GPU N), created on first use.
+constexpr int kMaxDevices = 64;
 kvsep_crc32c_ctx* default_ctx() {
-  static std::once_flag once;
-  static kvsep_crc32c_ctx* ctx = nullptr;
-  std::call_once(once, [] {
-    if (kvsep_crc32c_ctx_create(0, &ctx) != KVSEP_OK) {
-      std::fprintf(stderr, "kvsep_crc32c: GPU offload unavailable: %s\n", kvsep_last_error());
-      ctx = nullptr;
+  static std::once_flag once[kMaxDevices];
+  static kvsep_crc32c_ctx* ctx[kMaxDevices] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (dev < 0 || dev >= kMaxDevices) return nullptr;
+  std::call_once(once[dev], [dev] {
+    if (kvsep_crc32c_ctx_create(dev, &ctx[dev]) != KVSEP_OK) {
+      std::fprintf(stderr, "kvsep_crc32c: GPU offload unavailable on device %d: %s\n", dev, kvsep_last_error());
+      ctx[dev] = nullptr;
     }
   });
-  return ctx;
+  return ctx[dev];
 }
 
 }  // namespace
@@ -343,7 +372,7 @@ int host_copy_parallel(kvsep_crc32c_ctx* c, char* const* dst, const char* const*
   for (uint64_t i = 0; i < count; ++i)
     if (n[i]) segs.push_back({reinterpret_cast<uint8_t*>(dst[i]), reinterpret_cast<const uint8_t*>(src[i]), n[i]});
   std::lock_guard<std::mutex> g(ctx_mutex(c));
-  if (ensure_staging(c) != KVSEP_OK || !ctx_staging(c).pool) {
+  if (ensure_staging(c) != KVSEP_OK || !ctx_staging(c).pool) {  // no staging: the copies run on this thread
     for (auto& sg : segs) std::memcpy(sg.dst, sg.src, sg.n);
     return KVSEP_OK;
   }
@@ -418,6 +447,8 @@ int kvsep_crc32c_batch_host_span(kvsep_crc32c_ctx* c, const char* host_base, uin
   std::lock_guard<std::mutex> g(ctx_mutex(c));
   int rc = ensure_staging(c);
   if (rc) return rc;
+  DeviceGuard dg(ctx_device(c));
+  if (dg.err != hipSuccess) return hip_fail("hipSetDevice", dg.err);
   HostStaging& s = ctx_staging(c);
   const uint8_t* base = reinterpret_cast<const uint8_t*>(host_base);
   const bool pinned = span_bytes && is_pinned(host_base);
@@ -477,6 +508,8 @@ int kvsep_crc32c_batch_host(kvsep_crc32c_ctx* c, const uint32_t* init, const cha
   std::lock_guard<std::mutex> g(ctx_mutex(c));
   int rc = ensure_staging(c);
   if (rc) return rc;
+  DeviceGuard dg(ctx_device(c));
+  if (dg.err != hipSuccess) return hip_fail("hipSetDevice", dg.err);
   HostStaging& s = ctx_staging(c);
   SlotJob jobs[HostStaging::kSlots];
   int slot = 0;

@@ -65,7 +65,7 @@ uint64_t kvsep_vlog_walk(const char* buf, uint64_t n, uint64_t* off, uint64_t* l
 }
 
 int kvsep_vlog_verify_host(kvsep_crc32c_ctx* ctx, const char* buf, uint64_t n, uint64_t* nrecords, uint64_t* ngood,
-                           uint64_t* good_bytes) {
+                           uint64_t* good_bytes, uint64_t* drop_bytes) {
   if (!ctx || (!buf && n)) return KVSEP_EINVAL;
   const uint64_t cnt = kvsep_vlog_walk(buf, n, nullptr, nullptr, nullptr, 0, nullptr);
   std::vector<uint64_t> off(cnt), len(cnt);
@@ -80,6 +80,7 @@ int kvsep_vlog_verify_host(kvsep_crc32c_ctx* ctx, const char* buf, uint64_t n, u
   if (nrecords) *nrecords = cnt;
   if (ngood) *ngood = g;
   if (good_bytes) *good_bytes = g ? off[g - 1] + len[g - 1] : 0;
+  if (drop_bytes) *drop_bytes = g < cnt ? len[g] : 0;  // drop_size = buffer_.size() = the payload (:117-120)
   return KVSEP_OK;
 }
 

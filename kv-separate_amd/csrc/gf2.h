@@ -76,5 +76,22 @@ inline void byte_tables(const Mat32& m, uint32_t* out) {
     for (uint32_t b = 0; b < 256; ++b) out[k * 256 + b] = apply(m, b << (8 * k));
 }
 
+// The same maps as polynomial products: in the reflected representation (bit 31 = x^0) the register is a
+// polynomial R(x) and Z_n(R) = R * x^(8n) mod P.  mulmod is the carry-less product mod P, bit by bit.
+inline uint32_t mulmod(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+  for (int i = 31; i >= 0; --i) {
+    if ((a >> i) & 1u) p ^= b;
+    b = (b >> 1) ^ (kPolyReflected & (0u - (b & 1u)));
+  }
+  return p;
+}
+
+// out[k] = x^(2^k) mod P, k < 64: Z_n of any n is a product of at most 64 of them (the device's gf2_shift).
+inline void x2n_table(uint32_t* out) {
+  out[0] = 0x40000000u;  // x^1
+  for (int k = 1; k < 64; ++k) out[k] = mulmod(out[k - 1], out[k - 1]);
+}
+
 }  // namespace gf2
 }  // namespace kvsep

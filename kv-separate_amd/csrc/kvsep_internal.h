@@ -16,8 +16,8 @@ namespace kvsep {
 // pipeline gives each staging slot its own Scratch so the two slots' batches overlap.
 struct Scratch {
   uint64_t cap_count = 0, cap_pieces = 0;
-  uint32_t* d_counts = nullptr;
-  uint32_t* d_pstart = nullptr;
+  uint64_t* d_counts = nullptr;
+  uint64_t* d_pstart = nullptr;
   uint32_t* d_pblk = nullptr;
   uint32_t* d_partial = nullptr;
   void* d_scan_tmp = nullptr;
@@ -63,9 +63,30 @@ struct HostStaging {
   Scratch scratch[kSlots];
   CopyPool* pool = nullptr;
   bool ready = false;
+  bool failed = false;  // allocation failed once: not retried (ensure_staging)
 };
 
 void release_staging(HostStaging& s);
+
+// Makes `dev` the calling thread's current HIP device for the scope and restores the caller's device on every
+// exit path: the library never leaves a thread on another GPU than the one it came in with.
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) {
+      (void)hipGetLastError();
+      prev = -1;
+    }
+    if (prev != dev) err = hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int now = -1;
+    if (prev >= 0 && hipGetDevice(&now) == hipSuccess && now != prev) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
 
 // Implemented in crc32c_device.hip; callers hold ctx_mutex.
 int device_batch_locked(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* base, const uint64_t* off,

@@ -57,6 +57,7 @@ _SIGS = {
     "kvsep_crc32c_ctx_destroy": (None, [ctypes.c_void_p]),
     "kvsep_crc32c_ctx_set_piece_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     "kvsep_crc32c_ctx_set_schedule": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "kvsep_crc32c_ctx_set_kernel": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "kvsep_crc32c_reserve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]),
     "kvsep_crc32c_ctx_set_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "kvsep_crc32c_ctx_get_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
@@ -80,7 +81,7 @@ _SIGS = {
     "kvsep_vlog_walk": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     "kvsep_vlog_verify_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
-                                              ctypes.c_void_p, ctypes.c_void_p]),
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "kvsep_vlog_frame_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                              ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     "kvsep_log_walk": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
@@ -143,11 +144,20 @@ def _buf(data):
     raise TypeError(type(data))
 
 
+def _checked_len(keep, n):
+    """n defaults to the whole buffer; a larger n would read past it."""
+    if n is None:
+        return keep.nbytes
+    if n < 0 or n > keep.nbytes:
+        raise ValueError(f"n = {n} outside the {keep.nbytes}-byte buffer")
+    return n
+
+
 # ------------------------------------------------------------------ scalar mirror of util/crc32c.h
 def extend(init_crc: int, data, n: int | None = None) -> int:
     """leveldb::crc32c::Extend (util/crc32c.h:17)."""
     p, keep = _buf(data)
-    n = keep.nbytes if n is None else n
+    n = _checked_len(keep, n)
     return lib().kvsep_crc32c_extend(init_crc & 0xFFFFFFFF, p, n)
 
 
@@ -168,7 +178,7 @@ def unmask(masked: int) -> int:
 
 def extend_host(init_crc: int, data, n: int | None = None) -> int:
     p, keep = _buf(data)
-    n = keep.nbytes if n is None else n
+    n = _checked_len(keep, n)
     return lib().kvsep_crc32c_extend_host(init_crc & 0xFFFFFFFF, p, n)
 
 
@@ -222,9 +232,18 @@ class Context:
         _check(lib().kvsep_crc32c_ctx_set_piece_bytes(self._h, n), "set_piece_bytes")
 
     def set_schedule(self, dynamic):
-        """True = guided dynamic, False = static, None = auto (guided only when long blocks are split)."""
-        v = -1 if dynamic is None else (1 if dynamic else 0)
+        """True = guided dynamic, False = static contiguous runs, "rr" = static round-robin items, None = auto
+        (guided only when long blocks are split)."""
+        v = -1 if dynamic is None else 2 if dynamic == "rr" else (1 if dynamic else 0)
         _check(lib().kvsep_crc32c_ctx_set_schedule(self._h, v), "set_schedule")
+
+    KERNELS = {"auto": 0, "wide": 1, "narrow": 2, "narrow16": 3, "narrow8": 4}
+
+    def set_kernel(self, kernel: str):
+        """Kernel choice for unsplit batches (kvsep_crc32c_ctx_set_kernel): "auto" (default), "wide", or the narrow
+        kernel whenever the max_len hint is <= 64 KiB ("narrow"; "narrow16" / "narrow8" pin its workgroup size).
+        Never changes a result."""
+        _check(lib().kvsep_crc32c_ctx_set_kernel(self._h, self.KERNELS[kernel]), "set_kernel")
 
     def reserve(self, count: int, total_bytes: int):
         _check(lib().kvsep_crc32c_reserve(self._h, count, total_bytes), "reserve")
@@ -300,13 +319,14 @@ class Context:
 
 
     # -- framings (vlog / log / SST call sites)
-    def vlog_verify(self, image):
-        """db/value_log_reader.cc:86-138 over a whole vlog image -> (records, good, good_bytes)."""
+    def vlog_verify(self, image, with_drop=False):
+        """db/value_log_reader.cc:86-138 over a whole vlog image -> (records, good, good_bytes), plus the byte count
+        reported with "checksum mismatch" (0 if none) when with_drop."""
         p, keep = _buf(image)
-        n, g, gb = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        n, g, gb, dr = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         _check(lib().kvsep_vlog_verify_host(self._h, p, keep.nbytes, ctypes.byref(n), ctypes.byref(g),
-                                            ctypes.byref(gb)), "kvsep_vlog_verify_host")
-        return n.value, g.value, gb.value
+                                            ctypes.byref(gb), ctypes.byref(dr)), "kvsep_vlog_verify_host")
+        return (n.value, g.value, gb.value, dr.value) if with_drop else (n.value, g.value, gb.value)
 
     def vlog_frame(self, payloads, out=None):
         """db/value_log_writer.cc:46-76 for a batch of payloads -> bytes of the framed records; with `out` (a

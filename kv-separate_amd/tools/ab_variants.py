@@ -19,6 +19,9 @@ import torch  # noqa: E402
 import kvsep  # noqa: E402
 from kvsep import workloads as W  # noqa: E402
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _diag  # noqa: E402,F401  -- variant "a" is the KVSEP_DIAG build (its default = the shipped kernels)
+
 
 def layout(cfg):
     if cfg.startswith("u"):  # "u<count>x<len>[s<stride>][f<first>]": uniform blocks (packed unless s), e.g. u4096x4096

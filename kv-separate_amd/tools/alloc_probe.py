@@ -38,10 +38,8 @@ def main():
         c.set_schedule(False)
         c.reserve(off.size, total)
         scheds["static"] = c
-        os.environ["KVSEP_CRC_STATIC_RR"] = "1"
         c = kvsep.Context(0)
-        del os.environ["KVSEP_CRC_STATIC_RR"]
-        c.set_schedule(False)
+        c.set_schedule("rr")
         c.reserve(off.size, total)
         scheds["static-rr"] = c
     for k in range(args.allocs):

@@ -12,6 +12,9 @@ import torch  # noqa: E402
 import kvsep  # noqa: E402
 from kvsep import workloads as W  # noqa: E402
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _diag  # noqa: E402,F401  -- KVSEP_CRC_VARIANT reaches only the KVSEP_DIAG build
+
 blen = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 count = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5

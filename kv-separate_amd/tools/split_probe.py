@@ -19,8 +19,8 @@ span = int(off[-1] + ln[-1])
 data = torch.empty(span + 64, dtype=torch.uint8, device=dev)
 kvsep.fill_splitmix64(data.data_ptr(), span, 7, 0)
 ctx = kvsep.Context(0)
-os.environ["KVSEP_NARROW"] = "0"
 wide_only = kvsep.Context(0)
+wide_only.set_kernel("wide")
 
 
 def timeit(c, o, n, max_len, reps=5):

@@ -74,14 +74,14 @@ int main() {
     if (kvsep_vlog_frame_host(ctx, ptr.data(), len.data(), pl.size(), img.data(), img.size(), &w) != 0 || w != need)
       ++failures;
     uint64_t n = 0, good = 0, gb = 0;
-    kvsep_vlog_verify_host(ctx, img.data(), img.size(), &n, &good, &gb);
+    kvsep_vlog_verify_host(ctx, img.data(), img.size(), &n, &good, &gb, nullptr);
     if (n != pl.size() || good != n || gb != img.size()) ++failures;
     if (!img.empty()) {
       img[rng() % img.size()] ^= char(1 + rng() % 255);
       img.resize(rng() % (img.size() + 1));
     }
     std::vector<char> heap(img.begin(), img.end());  // exact-size heap buffer: ASan sees any over-read
-    kvsep_vlog_verify_host(ctx, heap.data(), heap.size(), &n, &good, &gb);
+    kvsep_vlog_verify_host(ctx, heap.data(), heap.size(), &n, &good, &gb, nullptr);
     if (good > n || gb > heap.size()) ++failures;
     // random bytes through the log/MANIFEST walker (32 KiB block framing)
     std::vector<char> junk(rng() % 70000);

@@ -55,7 +55,7 @@ int main(int argc, char** argv) {
   CHECK(f && std::fread(img, 1, wrote, f) == wrote);
   std::fclose(f);
   uint64_t records = 0, good = 0, good_bytes = 0;
-  CHECK(kvsep_vlog_verify_host(ctx, img, wrote, &records, &good, &good_bytes) == KVSEP_OK);
+  CHECK(kvsep_vlog_verify_host(ctx, img, wrote, &records, &good, &good_bytes, nullptr) == KVSEP_OK);
   CHECK(records == uint64_t(n) && good == uint64_t(n) && good_bytes == wrote);
 
   // the host scalar drop-in agrees with every stored header (util/crc32c.h:17 semantics)
@@ -71,7 +71,7 @@ int main(int argc, char** argv) {
   uint64_t off40 = 0;
   for (int i = 0; i < 40; ++i) off40 += 8 + len[i];
   img[off40 + 8 + 12345] ^= 0x80;
-  CHECK(kvsep_vlog_verify_host(ctx, img, wrote, &records, &good, &good_bytes) == KVSEP_OK);
+  CHECK(kvsep_vlog_verify_host(ctx, img, wrote, &records, &good, &good_bytes, nullptr) == KVSEP_OK);
   CHECK(records == uint64_t(n) && good == 40 && good_bytes == off40);
 
   kvsep_host_free_pinned(img);

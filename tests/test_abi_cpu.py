@@ -18,6 +18,35 @@ def test_library_exports_every_header_symbol():
     assert not missing, missing
 
 
+def test_exports_leveldb_extend_cpp_symbol():
+    """The link-level boundary: leveldb::crc32c::Extend(uint32_t, const char*, size_t) with C++ linkage
+    (util/crc32c.h:17), so a KVDB build keeps its own util/crc32c.h and only swaps util/crc32c.cc for the library."""
+    l = ctypes.CDLL(kvsep.LIB_PATH)
+    f = getattr(l, "_ZN7leveldb6crc32c6ExtendEjPKcm")
+    f.restype = ctypes.c_uint32
+    f.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]
+    assert f(0, b"123456789", 9) == 0xE3069283
+    assert f(0, b"TestCRCBuffer", 13) == 0xDCBC59FA  # util/crc32c.cc:267-274 self-test
+    assert f(0x12345678, None, 0) == 0x12345678
+
+
+def test_no_environment_variable_reaches_the_kernel_choice():
+    """The shipped library reads no variant / kernel-routing variable (those exist only in the KVSEP_DIAG tools
+    build): only KVSEP_STRICT_GPU and KVSEP_COPY_THREADS, neither of which can change a CRC."""
+    import re
+    strings = open(kvsep.LIB_PATH, "rb").read()
+    names = set(re.findall(rb"KVSEP_[A-Z_]{3,}", strings))
+    assert names <= {b"KVSEP_STRICT_GPU", b"KVSEP_COPY_THREADS"}, names
+
+
+def test_python_extend_rejects_n_past_buffer():
+    with pytest.raises(ValueError):
+        kvsep.extend(0, b"abc", 4)
+    with pytest.raises(ValueError):
+        kvsep.extend_host(0, b"abc", 5)
+    assert kvsep.extend(0, b"abc", 3) == kvsep.value(b"abc")
+
+
 def test_binding_covers_header():
     assert set(kvsep.header_functions()) <= set(kvsep._SIGS), set(kvsep.header_functions()) - set(kvsep._SIGS)
 

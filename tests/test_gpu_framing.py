@@ -39,8 +39,10 @@ def test_vlog_recovery_scan(ctx, oracle):
     bad = bytearray(img)
     off, ln, _, _ = kvsep.vlog_walk(img)
     bad[int(off[123]) + int(ln[123]) // 2] ^= 0x80        # corruption_test.cc-style flip in record 123
-    n, good, gb = ctx.vlog_verify(bytes(bad))
+    n, good, gb, drop = ctx.vlog_verify(bytes(bad), with_drop=True)
     assert (n, good) == (len(pl), 123) and gb == int(off[122] + ln[122])
+    assert drop == int(ln[123])  # VlogReader's drop_size for "checksum mismatch" (db/value_log_reader.cc:117-120)
+    assert ctx.vlog_verify(img, with_drop=True)[3] == 0
     n, good, gb = ctx.vlog_verify(img[:-5])              # torn tail: the last record is eof, not corrupt
     assert n == good == len(pl) - 1
 

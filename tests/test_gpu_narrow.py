@@ -1,9 +1,8 @@
 """GPU parity of the narrow kernel (8 lanes per block, 8 blocks per wavefront), which serves unsplit batches
 of many short blocks (SST blocks, WAL fragments; routing rule use_narrow() in crc32c_device.hip), forced here
 for every batch whose max_len hint is <= 64 KiB.  Bit-exact vs the oracle restatement and
-vs the wide kernel (KVSEP_NARROW=0 context), on ragged lengths, any alignment, non-zero init, partial
+vs the wide kernel (set_kernel("wide") context), on ragged lengths, any alignment, non-zero init, partial
 8-block groups and verify mode."""
-import os
 
 import numpy as np
 import pytest
@@ -23,17 +22,10 @@ NARROW_MAX = 64 * 1024
 
 @pytest.fixture(scope="module")
 def ctxs():
-    old = os.environ.get("KVSEP_NARROW")
-    try:
-        os.environ["KVSEP_NARROW"] = "7"  # narrow kernel whenever max_len <= 64 KiB (the default routes by count)
-        narrow = kvsep.Context(0)
-        os.environ["KVSEP_NARROW"] = "0"
-        wide = kvsep.Context(0)
-    finally:
-        if old is None:
-            del os.environ["KVSEP_NARROW"]
-        else:
-            os.environ["KVSEP_NARROW"] = old
+    narrow = kvsep.Context(0)
+    narrow.set_kernel("narrow")  # narrow kernel whenever max_len <= 64 KiB (the default routes by count)
+    wide = kvsep.Context(0)
+    wide.set_kernel("wide")
     yield narrow, wide
     narrow.close()
     wide.close()
