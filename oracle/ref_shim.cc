@@ -59,3 +59,68 @@ extern "C" int ref_crc32c_batch(const char* base, const uint64_t* off, const uin
   for (int t = 0; t < launched; ++t) pthread_join(th[t], nullptr);
   return 0;
 }
+
+// Full-size golden vectors (tests/golden/make_fullsize_golden.py): out[i] = reference Extend(0, block i) where block
+// i is bytes [stream_base + off[i], + len[i]) of the repo's splitmix64 stream `seed` (kvsep/workloads.py), generated
+// on the fly into a per-thread buffer at the block's own alignment mod 16, so whole BASELINE batches (64 GiB ..
+// 512 GiB) are checksummed by the reference without holding them in memory.  Threads take contiguous,
+// byte-balanced block ranges.
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+namespace {
+inline uint64_t sm_word(uint64_t seed, uint64_t j) {
+  uint64_t z = seed + (j + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+struct StreamJob {
+  uint64_t seed, base;
+  const uint64_t* off; const uint64_t* len; uint32_t* out;
+  size_t lo, hi;
+};
+void* stream_worker(void* p) {
+  StreamJob* j = static_cast<StreamJob*>(p);
+  uint64_t maxlen = 0;
+  for (size_t i = j->lo; i < j->hi; ++i) maxlen = j->len[i] > maxlen ? j->len[i] : maxlen;
+  std::vector<uint64_t> words((maxlen + 32) / 8 + 2);
+  std::vector<char> buf(maxlen + 32);
+  for (size_t i = j->lo; i < j->hi; ++i) {
+    const uint64_t g0 = j->base + j->off[i], n = j->len[i];
+    const uint64_t nw = (n + (g0 & 7) + 7) / 8;
+    for (uint64_t k = 0; k < nw; ++k) words[k] = sm_word(j->seed, (g0 >> 3) + k);  // little-endian host
+    char* at = buf.data() + (j->off[i] & 15);
+    std::memcpy(at, reinterpret_cast<const char*>(words.data()) + (g0 & 7), n);
+    j->out[i] = leveldb::crc32c::Extend(0, at, n);
+  }
+  return nullptr;
+}
+}  // namespace
+
+extern "C" int ref_crc32c_stream_batch(uint64_t seed, uint64_t stream_base, const uint64_t* off, const uint64_t* len,
+                                       size_t count, uint32_t* out, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  uint64_t total = 0;
+  for (size_t i = 0; i < count; ++i) total += len[i];
+  pthread_t th[256];
+  StreamJob jobs[256];
+  size_t start = 0;
+  uint64_t acc = 0;
+  int launched = 0;
+  for (int t = 0; t < nthreads && start < count; ++t) {
+    const uint64_t target = (total / uint64_t(nthreads)) * uint64_t(t + 1);
+    size_t stop = start;
+    if (t == nthreads - 1) stop = count;
+    else
+      while (stop < count && acc < target) acc += len[stop++];
+    jobs[t] = StreamJob{seed, stream_base, off, len, out, start, stop};
+    if (pthread_create(&th[t], nullptr, stream_worker, &jobs[t]) != 0) return -1;
+    ++launched;
+    start = stop;
+  }
+  for (int t = 0; t < launched; ++t) pthread_join(th[t], nullptr);
+  return 0;
+}

@@ -91,3 +91,52 @@ def test_oracle_batch_threads_agree(oracle):
     off, ln = W.cfg4_layout(2000)
     data = splitmix64_bytes(int(off[-1] + ln[-1]), 7, 0)
     assert np.array_equal(oracle.batch(data, off, ln, threads=1), oracle.batch(data, off, ln, threads=8))
+
+
+# ---------------------------------------------------------------- full-size reference files (make_fullsize_golden.py)
+import os  # noqa: E402
+
+_GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _full(name):
+    return np.fromfile(os.path.join(_GOLDEN_DIR, name), dtype="<u4")
+
+
+def test_fullsize_files_agree_with_the_small_fixtures(golden):
+    c2, c5, c4, c3a = _full("full_cfg2.u32"), _full("full_cfg5.u32"), _full("full_cfg4.u32"), _full("full_cfg3a.u32")
+    assert (c2.size, c3a.size, c5.size, c4.size) == (65536, 65536, 8 * 65536, 1 << 20)
+    g2 = golden["cfg2"]
+    assert c2[:256].tolist() == g2["first"]
+    assert int(np.bitwise_xor.reduce(c2)) == g2["xor"] and int(c2.astype(np.uint64).sum()) == g2["sum"]
+    assert c5[:32].tolist() == golden["cfg3b"]["crc"]          # slice 0 of config 5 is config 3b
+    assert c4[:512].tolist() == golden["cfg4"]["crc"]
+
+
+def _oracle_blocks(oracle, seed, base, off, ln, idx):
+    out = []
+    for i in idx:
+        d = splitmix64_bytes(int(ln[i]), seed, base + int(off[i]))
+        out.append(oracle.extend_addr(0, d.ctypes.data, d.size))
+    return out
+
+
+def test_oracle_matches_fullsize_reference_samples(oracle):
+    """The restatement against the reference's whole-batch outputs, on blocks spread over each batch (config 5:
+    every slice, i.e. stream offsets up to 448 GiB)."""
+    rng = np.random.default_rng(7)
+    off, ln = W.cfg3_layout()
+    idx = rng.integers(0, off.size, 6)
+    assert _oracle_blocks(oracle, W.SEED + 1, 0, off, ln, idx) == _full("full_cfg3a.u32")[idx].tolist()
+    off, ln = W.cfg3_layout(vlog=True)
+    span = int(off[-1] + ln[-1])
+    c5 = _full("full_cfg5.u32")
+    for s in range(8):
+        idx = rng.integers(0, off.size, 2)
+        assert _oracle_blocks(oracle, W.SEED + 1, s * span, off, ln, idx) == c5[s * off.size + idx].tolist(), s
+    off, ln = W.cfg4_layout()
+    idx = np.concatenate([rng.integers(0, off.size, 24), [off.size - 1]])
+    assert _oracle_blocks(oracle, W.SEED + 2, 0, off, ln, idx) == _full("full_cfg4.u32")[idx].tolist()
+    off, ln = W.cfg2_layout()
+    idx = rng.integers(0, off.size, 64)
+    assert _oracle_blocks(oracle, W.SEED, 0, off, ln, idx) == _full("full_cfg2.u32")[idx].tolist()
