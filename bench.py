@@ -1,15 +1,22 @@
 #!/usr/bin/env python3
 """bench.py -- CRC32C GiB/s, device-resident, batched 1 MiB blocks (BASELINE.json metric).
 
-One step = one pass of the CRC engine (libkvsep_crc32c, C ABI) over one batch that already sits in
-HBM: config 3 of BASELINE.json, 65,536 x 1 MiB blocks (64 GiB) per GPU (`--config 3a`, default);
-`--config 3b` is the vlog-framed variant (1,048,609-B payloads at 8 + i*(8+len): odd offsets),
-`2` is 65,536 x 4 KiB, `4` the Zipf ragged batch.  N > 1: one process per GPU (torchrun), each rank
-checksums its own shard (weak scaling, no data-path collective); rank 0 prints one JSON line.
+One step = one pass of the CRC engine (libkvsep_crc32c, C ABI) over one batch that already sits in HBM:
+config 3 of BASELINE.json, 65,536 x 1 MiB blocks (64 GiB) per GPU (`--config 3a`, default).  Other configs:
+  3b  the vlog-framed variant (1,048,609-B payloads at 8 + i*(8+len): odd offsets)
+  2   65,536 x 4 KiB SST blocks
+  4   the ragged Zipf batch: ONE global batch of N x 2^20 blocks cut into byte-balanced contiguous block ranges
+      (kvsep_crc32c_partition), one per rank -- at N = 1 exactly config 4
+  5   the 512 GiB vlog (524,288 x 1,048,609-B records) split over the N ranks (strong scaling): each rank owns
+      8/N distinct 64 GiB slices; with more than one, every pass regenerates its slice in HBM at its true stream
+      offset outside the timed region, so all 512 GiB checksummed are distinct data
+N > 1: one process per GPU (torchrun), each rank checksums its own shard; no data-path collective.
 
-Outside the timed region: RCCL all-gather of each rank's CRC-of-CRCs digest, a parity spot check
-against the oracle (test infrastructure), the read-only streaming ceiling, the host round-trip rate
-and -- rank 0 at N = 1 -- the oracle's CPU throughput on a bounded sample (cpu_baseline).
+Outside the timed region: RCCL all-gather of every rank's u32 results (4 B per block) and a check of EVERY block
+against the reference's whole-batch outputs (tests/golden/full_cfg*.u32, computed by the compiled util/crc32c.cc)
+where they cover it, an oracle recompute of sampled blocks elsewhere; the read-only streaming ceiling; the host
+round-trip rate; and -- rank 0 at N = 1 -- the compiled reference's CPU throughput on a bounded sample
+(cpu_baseline) at 1 thread and at every core this process may run on.
 """
 from __future__ import annotations
 
@@ -34,26 +41,76 @@ from kvsep import workloads as W  # noqa: E402
 
 GIB = float(1 << 30)
 HBM_PEAK_GBPS = 8000.0  # MI355X spec HBM3E peak (MI355X_MICROARCH.md: 8.0 TB/s)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+METRIC = "CRC32C GiB/s device-resident, batched 1 MiB blocks, 1/2/4/8 MI355X"
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def layout(cfg: str):
-    if cfg == "3a":
-        off, ln = W.cfg3_layout()
-        return off, ln, "65536 x 1 MiB blocks, 16-B aligned (config 3, variant A)"
-    if cfg == "3b":
-        off, ln = W.cfg3_layout(vlog=True)
-        return off, ln, "65536 x 1,048,609-B vlog payloads at 8 + i*(8+len) (config 3, variant B)"
-    if cfg == "2":
-        off, ln = W.cfg2_layout()
-        return off, ln, "65536 x 4 KiB SST blocks (config 2)"
-    if cfg == "4":
-        off, ln = W.cfg4_layout()
-        return off, ln, "1,048,576 Zipf(1.1) blocks, 32 B - 4 MiB (config 4)"
-    raise SystemExit(f"unknown config {cfg}")
+_CFG4 = {}
+
+
+def _cfg4_global(world):
+    """Config 4 over `world` ranks: one packed batch of world x 2^20 Zipf blocks (its first 2^20 ARE config 4)."""
+    if world not in _CFG4:
+        glen = W.zipf_lengths(world * W.CFG4_BLOCKS)
+        goff = np.zeros(glen.size, np.uint64)
+        goff[1:] = np.cumsum(glen[:-1], dtype=np.uint64)
+        _CFG4[world] = (goff, glen)
+    return _CFG4[world]
+
+
+class Plan:
+    """What this rank checksums: a local block layout over one buffer, and one (stream_base, index_base) per pass
+    -- the global stream offset of the buffer's first byte and the global index of its first block."""
+
+    def __init__(self, cfg: str, world: int, rank: int):
+        self.cfg = cfg
+        self.passes = [(0, 0)]
+        self.golden = None  # (file, seed): reference per-block CRCs of the global batch, indexed globally
+        if cfg in ("2", "3a", "3b"):
+            if cfg == "2":
+                self.off, self.ln = W.cfg2_layout()
+                self.seed, self.golden = W.SEED, "full_cfg2.u32"
+                self.desc = "65536 x 4 KiB SST blocks (config 2)"
+            elif cfg == "3a":
+                self.off, self.ln = W.cfg3_layout()
+                self.seed, self.golden = W.SEED + 1, "full_cfg3a.u32"
+                self.desc = "65536 x 1 MiB blocks, 16-B aligned (config 3, variant A)"
+            else:
+                self.off, self.ln = W.cfg3_layout(vlog=True)
+                self.seed, self.golden = W.SEED + 1, "full_cfg5.u32"  # rank r = slice r of the 512 GiB vlog
+                self.desc = "65536 x 1,048,609-B vlog payloads at 8 + i*(8+len) (config 3, variant B)"
+            span = int(self.off[-1] + self.ln[-1])
+            self.passes = [(shard.stream_offset(rank, span), rank * self.off.size)]
+            self.scaling = "weak"
+        elif cfg == "4":
+            goff, glen = _cfg4_global(world)
+            self.off, self.ln, base, ib = shard.partition_layout(goff, glen, world, rank)
+            self.passes = [(base, ib)]
+            self.seed, self.golden = W.SEED + 2, "full_cfg4.u32"
+            self.desc = (f"{world} x 1,048,576 Zipf(1.1) blocks, 32 B - 4 MiB, one batch cut into byte-balanced block "
+                         f"ranges (config 4)")
+            self.scaling = "weak"
+        elif cfg == "5":
+            if 8 % world:
+                raise SystemExit("--config 5 needs 1, 2, 4 or 8 ranks")
+            per = 8 // world
+            self.off, self.ln = W.cfg3_layout(vlog=True)
+            span = int(self.off[-1] + self.ln[-1])
+            slices = [rank * per + p for p in range(per)]
+            self.passes = [(s * span, s * self.off.size) for s in slices]
+            self.seed, self.golden = W.SEED + 1, "full_cfg5.u32"
+            self.desc = (f"512 GiB vlog batch (524,288 x 1,048,609-B records) over {world} GPU(s): {per} distinct "
+                         f"64 GiB slice(s) per GPU (config 5)")
+            self.scaling = "strong"
+        else:
+            raise SystemExit(f"unknown config {cfg}")
+        self.count = int(self.off.size)
+        self.useful = int(self.ln.sum())
+        self.span = int(self.off[-1] + self.ln[-1]) if self.count else 0
 
 
 def to_dev_u64(a, dev):
@@ -86,9 +143,20 @@ class RefBatch:
         return out
 
 
-def cpu_baseline(oracle, data_dev, off, ln, sample_blocks, threads, seconds):
-    """CPU CRC on host cores over a sample of the batch: the compiled reference (kind "reference")
-    when oracle/_ref was built, else the oracle restatement (kind "port")."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(oracle, data_dev, off, ln, sample_blocks, thread_counts, seconds):
+    """CPU CRC on host cores over a sample of the batch: the compiled reference (kind "reference") when oracle/_ref
+    was built, else the oracle restatement (kind "port"), at each thread count in `thread_counts`."""
     idx = np.linspace(0, off.size - 1, sample_blocks).astype(np.int64)
     lens = ln[idx]
     host = np.empty(int(lens.sum()), dtype=np.uint8)
@@ -103,7 +171,7 @@ def cpu_baseline(oracle, data_dev, off, ln, sample_blocks, threads, seconds):
     impl, kind = oracle, "port"
     if os.path.exists(RefBatch.PATH):
         impl, kind = RefBatch(), "reference"
-    for t in sorted({1, threads}):
+    for t in thread_counts:
         sub = sample_blocks if t > 1 else max(1, sample_blocks // 4)
         sb = int(lens[:sub].sum())
         impl.batch(host, hoff[:min(sub, 8)], lens[:min(sub, 8)], threads=1)  # warm tables
@@ -119,17 +187,6 @@ def cpu_baseline(oracle, data_dev, off, ln, sample_blocks, threads, seconds):
     return out, host, hoff, lens, idx, kind
 
 
-def cpu_model() -> str:
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return "unknown"
-
-
 def sse42_rate(host, hoff, lens, threads, seconds):
     """Informational: the library's own SSE4.2 `crc32` host leg (the drop-in's small-input path, i.e. the
     "accelerated" CPU path google/crc32c would give the reference) over the same host sample; GiB/s."""
@@ -137,7 +194,6 @@ def sse42_rate(host, hoff, lens, threads, seconds):
     base = host.ctypes.data
     items = [(base + int(o), int(n)) for o, n in zip(hoff, lens)]
     parts = [items[t::threads] for t in range(threads)]
-    total = sum(n for _, n in items)
     fn(0, items[0][0], min(items[0][1], 4096))  # warm
 
     def work(part, stop_at, acc):
@@ -156,8 +212,7 @@ def sse42_rate(host, hoff, lens, threads, seconds):
     for th in ths:
         th.join()
     dt = time.perf_counter() - t0
-    done = sum(sum(a) for a in accs)
-    return done / GIB / dt, total
+    return sum(sum(a) for a in accs) / GIB / dt
 
 
 def roundtrip_setup(ctx, nbytes_target: int):
@@ -188,6 +243,30 @@ def roundtrip_time(ctx, state, reps=3):
     return (time.perf_counter() - t0) / reps, bool(np.array_equal(res, ref))
 
 
+def check_results(plan_all, results, oracle):
+    """Every rank's u32 results (gathered) against the reference's whole-batch outputs where they cover the block's
+    global index, an oracle recompute of 16 sampled blocks per (rank, pass) elsewhere.  Rank 0, untimed."""
+    checked = mism = sampled = 0
+    gold_cache = {}
+    for plan, res in zip(plan_all, results):
+        k = plan.count
+        gold = None
+        if plan.golden:
+            gold = gold_cache.setdefault(plan.golden, np.fromfile(os.path.join(GOLDEN, plan.golden), dtype="<u4"))
+        for p, (base, ib) in enumerate(plan.passes):
+            got = res[p * k:(p + 1) * k]
+            n_gold = 0 if gold is None else max(0, min(k, gold.size - ib))
+            if n_gold:
+                mism += int(np.count_nonzero(got[:n_gold] != gold[ib:ib + n_gold]))
+                checked += n_gold
+            rest = np.arange(n_gold, k)
+            for i in rest[np.linspace(0, rest.size - 1, min(16, rest.size)).astype(np.int64)] if rest.size else []:
+                d = kvsep.splitmix64_bytes(int(plan.ln[i]), plan.seed, base + int(plan.off[i]))
+                mism += int(oracle.extend_addr(0, d.ctypes.data, d.size) != int(got[i]))
+                sampled += 1
+    return {"blocks_checked_vs_reference": checked, "blocks_sampled_vs_oracle": sampled, "mismatches": mism}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -204,8 +283,8 @@ def main():
                     help="steps captured per hipGraph (0 = all timed steps in one graph when --steps <= 64, so the "
                          "GPU runs them back to back; 1 = one replay per step)")
     ap.add_argument("--cpu-sample-blocks", type=int, default=4096)
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU work per thread count (>= 1 pass)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may run on")
+    ap.add_argument("--cpu-seconds", type=float, default=5.0, help="CPU work per thread count (>= 1 pass)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--roundtrip-gib", type=float, default=4.0)
     ap.add_argument("--pmc-json", default=None,
@@ -224,6 +303,7 @@ def main():
         else:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dd = dist if world > 1 else None
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     coll_dev = dev if world == 1 or dist.get_backend() == "nccl" else torch.device("cpu")
@@ -234,110 +314,135 @@ def main():
     if args.schedule != "default":
         ctx.set_schedule(args.schedule == "dynamic")
 
-    passes = 1
-    if args.config == "5":
-        # Config 5: ONE 512 GiB vlog batch (524,288 records of 1,048,609 B, variant-B framing) split over the
-        # ranks.  512 GiB exceeds one GPU's HBM, so each rank keeps a 64 GiB slice of records resident and a
-        # step runs 8/N passes over it (each pass reads all 64 GiB from HBM again; nothing is cached at
-        # this size).  Total work per step is fixed: strong scaling.
-        if 8 % world:
-            raise SystemExit("--config 5 needs 1, 2, 4 or 8 ranks")
-        passes = 8 // world
-        off, ln, _ = layout("3b")
-        desc = (f"512 GiB vlog batch (524,288 x 1,048,609-B records) over {world} GPU(s): {passes} pass(es) "
-                f"of a resident 64 GiB slice per GPU (config 5)")
-    else:
-        off, ln, desc = layout(args.config)
-    count = int(off.size)
-    useful = int(ln.sum())
-    span = int(off[-1] + ln[-1])
-    max_len = 0 if args.no_plan_hint else int(ln.max())
-    log(f"[rank {rank}] {desc}: {useful / GIB:.2f} GiB useful, span {span / GIB:.2f} GiB")
+    plan = Plan(args.config, world, rank)
+    off, ln, count, useful, span = plan.off, plan.ln, plan.count, plan.useful, plan.span
+    npass = len(plan.passes)
+    max_len = 0 if args.no_plan_hint else (int(ln.max()) if count else 0)
+    log(f"[rank {rank}] {plan.desc}: {useful / GIB:.2f} GiB useful per pass x {npass}, span {span / GIB:.2f} GiB")
 
-    # synthetic data, generated in HBM: rank r holds bytes [r*span, (r+1)*span) of one stream
+    # synthetic data, generated in HBM: the buffer holds global stream bytes [stream_base, stream_base + span)
     data = torch.empty(span + 64, dtype=torch.uint8, device=dev)
-    seed = W.SEED + (1 if args.config[0] in "35" else 2 if args.config == "4" else 0)
-    kvsep.fill_splitmix64(data.data_ptr(), span, seed, shard.stream_offset(rank, span))
+
+    def fill(p):
+        kvsep.fill_splitmix64(data.data_ptr(), span, plan.seed, plan.passes[p][0])
+
+    fill(0)
     d_off, d_len = to_dev_u64(off, dev), to_dev_u64(ln, dev)
-    out = torch.zeros(count, dtype=torch.int32, device=dev)
+    out = torch.zeros((npass, max(count, 1)), dtype=torch.int32, device=dev)
     ctx.reserve(count, useful)
     stream = torch.cuda.current_stream()
 
-    def step(st):
-        for _ in range(passes):
-            ctx.batch_device(data.data_ptr(), d_off, d_len, out, count=count, total_bytes=useful, max_len=max_len,
-                             stream=st)
+    def crc(p, st):
+        ctx.batch_device(data.data_ptr(), d_off, d_len, out[p], count=count, total_bytes=useful, max_len=max_len,
+                         stream=st)
 
+    # ---- warm-up
     for _ in range(args.warmup):
-        step(stream)
-    torch.cuda.synchronize()
-    # kernel-only time of the CRC kernel, HIP events on the stream it runs on.  A step of an unsplit batch is the
-    # CRC kernel alone: under graph replay, one event pair around the timed region gives its average over the
-    # back-to-back launches.  A split batch also runs planning and combine kernels, so its CRC kernel is timed
-    # with an event pair per launch over the same number of eager steps.
-    piece = args.piece_kib * 1024 or kvsep.DEFAULT_PIECE_BYTES
-    span_timing = args.launch == "graph" and passes == 1 and 0 < max_len <= piece
-    ctx.get_timing()
-    ctx.set_timing(True)
-    for _ in range(args.steps if args.launch == "graph" and not span_timing else 0):
-        step(stream)
+        for p in range(npass):
+            if npass > 1:
+                fill(p)
+            crc(p, stream)
     torch.cuda.synchronize()
 
-    # the timed steps as hipGraph replays: each captured step is a full pass of the hot path (planning kernels,
-    # memsets, CRC kernel(s), combine; kvsep_crc32c_reserve made every allocation beforehand).  By default all K
-    # timed steps are captured into ONE graph, so the GPU runs them back to back instead of waiting on a host
-    # replay per step (a 50 us config-2 step otherwise pays ~7 us of replay turnaround); or eager launches.
-    run = lambda: step(stream)  # noqa: E731
+    piece = args.piece_kib * 1024 or kvsep.DEFAULT_PIECE_BYTES
+    graphable = npass == 1
+    span_timing = args.launch == "graph" and graphable and 0 < max_len <= piece
     launch = "eager"
-    n_calls = args.steps
-    if args.launch == "graph":
-        ctx.set_timing(False)  # no timing events inside the graph
-        per = args.graph_steps or (args.steps if args.steps <= 64 else 1)
-        if args.steps % per:
-            per = 1
-        try:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for _ in range(per):
-                    step(torch.cuda.current_stream())
-            g.replay()  # warm replay
-            torch.cuda.synchronize()
-            run, launch, n_calls = g.replay, f"hipGraph ({per} step(s) per replay)", args.steps // per
-        except Exception as e:  # keep the measurement: fall back to eager launches
-            log(f"[rank {rank}] graph capture failed ({e}); timing eager launches")
-            torch.cuda.synchronize()
-            span_timing = False
-            ctx.set_timing(True)
     ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    if span_timing:
-        ev[0].record()  # the graph replays on the current stream
-    for _ in range(n_calls):
-        run()
-    if span_timing:
-        ev[1].record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    ctx.set_timing(False)
-    kern_ms, launches = ctx.get_timing()
-    if span_timing:
-        kern_ms, launches = ev[0].elapsed_time(ev[1]), args.steps
-    elapsed = shard.max_over_ranks(elapsed, dist if world > 1 else None, coll_dev)
+    if npass == 1:
+        # kernel-only time of the CRC kernel, HIP events on the stream it runs on.  A step of an unsplit batch is the
+        # CRC kernel alone: under graph replay, one event pair around the timed region gives its average over the
+        # back-to-back launches.  A split batch also runs planning and combine kernels, so its CRC kernel is timed
+        # with an event pair per launch over the same number of eager steps.
+        ctx.get_timing()
+        ctx.set_timing(True)
+        for _ in range(args.steps if args.launch == "graph" and not span_timing else 0):
+            crc(0, stream)
+        torch.cuda.synchronize()
+        # the timed steps as hipGraph replays: each captured step is a full pass of the hot path (planning kernels,
+        # memsets, CRC kernel(s), combine; kvsep_crc32c_reserve made every allocation beforehand).  By default all K
+        # timed steps are captured into ONE graph, so the GPU runs them back to back instead of waiting on a host
+        # replay per step (a 50 us config-2 step otherwise pays ~7 us of replay turnaround); or eager launches.
+        run = lambda: crc(0, stream)  # noqa: E731
+        n_calls = args.steps
+        if args.launch == "graph":
+            ctx.set_timing(False)  # no timing events inside the graph
+            per = args.graph_steps or (args.steps if args.steps <= 64 else 1)
+            if args.steps % per:
+                per = 1
+            try:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for _ in range(per):
+                        crc(0, torch.cuda.current_stream())
+                g.replay()  # warm replay
+                torch.cuda.synchronize()
+                run, launch, n_calls = g.replay, f"hipGraph ({per} step(s) per replay)", args.steps // per
+            except Exception as e:  # keep the measurement: fall back to eager launches
+                log(f"[rank {rank}] graph capture failed ({e}); timing eager launches")
+                torch.cuda.synchronize()
+                span_timing = False
+                ctx.set_timing(True)
+        if dd:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if span_timing:
+            ev[0].record()  # the graph replays on the current stream
+        for _ in range(n_calls):
+            run()
+        if span_timing:
+            ev[1].record()
+        torch.cuda.synchronize()
+        if dd:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        ctx.set_timing(False)
+        kern_ms, launches = ctx.get_timing()
+        if span_timing:
+            kern_ms, launches = ev[0].elapsed_time(ev[1]), args.steps
+        timing_note = ("one HIP event pair around the timed graph replay of back-to-back single-kernel steps"
+                       if span_timing else "a HIP event pair around each launch of the CRC kernel")
+    else:
+        # Config 5 with several distinct slices per GPU: a step is one CRC pass over each of this rank's slices.  A
+        # pass's slice is (re)generated in HBM before its timed region opens -- the data "arriving" -- so every
+        # timed pass starts with its input resident, like every other config; each pass is bracketed by barrier +
+        # synchronize, the step time is the sum of its passes.
+        elapsed = 0.0
+        ctx.get_timing()
+        for _ in range(args.steps):
+            for p in range(npass):
+                fill(p)
+                torch.cuda.synchronize()
+                if dd:
+                    dist.barrier()
+                ctx.set_timing(True)
+                t0 = time.perf_counter()
+                crc(p, stream)
+                torch.cuda.synchronize()
+                if dd:
+                    dist.barrier()
+                elapsed += time.perf_counter() - t0
+                ctx.set_timing(False)
+        kern_ms, launches = ctx.get_timing()
+        timing_note = ("a HIP event pair around each launch of the CRC kernel; each slice regenerated in HBM "
+                       "outside the timed passes")
+    elapsed = shard.max_over_ranks(elapsed, dd, coll_dev)
+    total_useful = useful * npass
+    if dd:
+        t = torch.tensor([total_useful], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t)
+        total_useful = int(t.item())
     ms_per_step = elapsed * 1e3 / args.steps
-    value = world * passes * useful * args.steps / GIB / elapsed
+    value = total_useful * args.steps / GIB / elapsed
     kern_avg_ms = kern_ms / max(1, launches)
     kernel_name = ctx.kernel_name(count, max_len)
     achieved_gbps = useful / (kern_avg_ms * 1e-3) / 1e9
 
-    # ---- outside the timed region: result digest gather (RCCL), parity spot check, ceilings
-    crcs = out.cpu().numpy().view(np.uint32)
-    digest = shard.crc_of_crcs(crcs, kvsep.extend_host)
-    digests = shard.gather_digests(digest, dist if world > 1 else None, coll_dev)
+    # ---- outside the timed region: u32 results of every rank gathered (RCCL), every block checked
+    crcs = out[:, :count].cpu().numpy().view(np.uint32).reshape(-1)
+    results = shard.gather_results(crcs, dd, coll_dev)
+    digests = [shard.crc_of_crcs(r, kvsep.extend_host) for r in results]
 
     read_ceiling_gbps = None  # the streaming kernel needs >= 1 MiB per wave to be a ceiling (8 GiB and up)
     if span >= 8 * (1 << 30):
@@ -356,35 +461,31 @@ def main():
     cpu = None
     if rank == 0:
         oracle = load_oracle()
-        threads = min(args.cpu_threads, len(os.sched_getaffinity(0)))
-        nsample = min(args.cpu_sample_blocks, count)
+        parity = check_results([Plan(args.config, world, r) for r in range(world)], results, oracle)
+        parity["all_blocks_match"] = parity["mismatches"] == 0
         if not args.no_cpu and world == 1:
-            res, host, hoff, lens, idx, kind = cpu_baseline(oracle, data, off, ln, nsample, threads,
-                                                            args.cpu_seconds)
-            exp = oracle.batch(host, hoff, lens, threads=threads)
-            parity = bool(np.array_equal(exp, crcs[idx]))
+            aff = len(os.sched_getaffinity(0))
+            threads = args.cpu_threads or aff
+            counts = sorted({1, min(16, threads), threads})
+            nsample = min(args.cpu_sample_blocks, count)
+            res, host, hoff, lens, idx, kind = cpu_baseline(oracle, data, off, ln, nsample, counts, args.cpu_seconds)
             vt, sbt, dtt = res[threads]
-            v1, sb1, dt1 = res[1]
             impl_desc = ("util/crc32c.cc of the reference (portable path, g++ -O3, oracle/_ref)"
                          if kind == "reference" else
                          "oracle/crc32c_oracle.c (restated util/crc32c.cc portable path, gcc -O3)")
             cpu = {"value": round(vt, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
                    "sample": f"{nsample} blocks of the same batch ({int(lens.sum()) / GIB:.2f} GiB) copied to host "
-                             f"memory, {impl_desc}; {threads} threads split by bytes: {sbt / GIB:.1f} GiB in "
-                             f"{dtt:.1f} s (repeated passes); 1 thread: {v1:.3f} GiB/s, {sb1 / GIB:.1f} GiB in "
-                             f"{dt1:.1f} s",
-                   "single_thread_GiBps": round(v1, 3), "cpu_model": cpu_model()}
-            s1, _ = sse42_rate(host, hoff[:max(1, nsample // 4)], lens[:max(1, nsample // 4)], 1, 2.0)
-            sn, _ = sse42_rate(host, hoff, lens, threads, 2.0)
+                             f"memory, {impl_desc}; blocks split over threads by bytes, repeated passes: "
+                             f"{threads} threads {sbt / GIB:.1f} GiB in {dtt:.1f} s",
+                   "by_threads_GiBps": {str(t): round(res[t][0], 3) for t in counts},
+                   "single_thread_GiBps": round(res[1][0], 3),
+                   "nproc": os.cpu_count(), "affinity_cores": aff, "cpu_model": cpu_model()}
+            s1 = sse42_rate(host, hoff[:max(1, nsample // 4)], lens[:max(1, nsample // 4)], 1, 2.0)
+            sn = sse42_rate(host, hoff, lens, threads, 2.0)
             cpu["sse42_crc32_GiBps"] = {"1": round(s1, 3), str(threads): round(sn, 3),
                                         "note": "informational, not the baseline: the library's SSE4.2 crc32 host "
                                                 "leg (3-way interleaved crc32q) on the same sample; the reference "
                                                 "build here has no accelerated path (HAVE_CRC32C=0)"}
-        else:
-            idx = np.linspace(0, count - 1, 16).astype(np.int64)
-            hostb = [data[int(off[i]):int(off[i] + ln[i])].cpu().numpy() for i in idx]
-            exp = [oracle.extend_addr(0, h.ctypes.data, h.size) for h in hostb]
-            parity = bool(list(crcs[idx]) == exp)
 
     # host round trip (PCIe-inclusive).  At N > 1 every rank streams its own pinned image through its own GPU
     # at the same time (each GPU has its own PCIe link); the rate is the sum over ranks / the slowest rank.
@@ -392,14 +493,13 @@ def main():
     rt = None
     rt_ok = None
     if args.roundtrip_gib > 0:
-        dd = dist if world > 1 else None
         state = None
         try:
             state = roundtrip_setup(ctx, int(args.roundtrip_gib * GIB))
         except Exception as e:  # keep the headline line even if pinned allocation is refused
             log(f"[rank {rank}] host round trip setup failed: {e}")
         if shard.min_over_ranks(1 if state is not None else 0, dd, coll_dev):
-            if world > 1:
+            if dd:
                 dist.barrier()
             dt, good = float("inf"), False
             try:
@@ -413,6 +513,7 @@ def main():
         state = None
 
     traffic = None
+    traffic_src = None
     pmc_cfg = "3b" if args.config == "5" else args.config  # config 5's launches are config-3b launches
     if args.pmc_json is None:
         args.pmc_json = os.path.join(ROOT, "profiles", f"pmc_cfg{pmc_cfg}.json")
@@ -421,12 +522,13 @@ def main():
             pm = json.load(open(args.pmc_json))
             if pm.get("config") == pmc_cfg:
                 traffic = pm.get("hbm_bytes_per_launch")
+                traffic_src = os.path.relpath(args.pmc_json, ROOT) + " (rocprofv3 --pmc passes of the same config)"
         except Exception:
             traffic = None
 
     if rank == 0:
         line = {
-            "metric": "CRC32C GiB/s device-resident, batched 1 MiB blocks, 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -435,19 +537,18 @@ def main():
             "ms_per_step": round(ms_per_step, 4),
             "launch": launch,
             "higher_is_better": True,
-            "scaling": "strong" if args.config == "5" else "weak",
+            "scaling": plan.scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 byte stream generated in HBM)",
-            "config": {"workload": desc, "config": args.config, "blocks_per_gpu": count * passes,
-                       "bytes_per_gpu": useful * passes, "piece_bytes": args.piece_kib * 1024 or kvsep.DEFAULT_PIECE_BYTES,
+            "config": {"workload": plan.desc, "config": args.config, "blocks_per_gpu": count * npass,
+                       "bytes_per_gpu": useful * npass, "total_bytes": total_useful,
+                       "piece_bytes": args.piece_kib * 1024 or kvsep.DEFAULT_PIECE_BYTES,
                        "parallelism": f"shard{world} (independent blocks per GPU, no data-path collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved_gbps / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel": kernel_name, "kernel_avg_ms": round(kern_avg_ms, 4),
-                         "kernel_timing": ("one HIP event pair around the timed graph replay of back-to-back "
-                                           "single-kernel steps" if span_timing else
-                                           "a HIP event pair around each launch of the CRC kernel"),
+                         "traffic_source": traffic_src,
+                         "kernel": kernel_name, "kernel_avg_ms": round(kern_avg_ms, 4), "kernel_timing": timing_note,
                          "algorithmic_bytes_per_launch": useful},
             "cpu_baseline": cpu,
             "read_ceiling_GBps": read_ceiling_gbps and round(read_ceiling_gbps, 1),
@@ -455,12 +556,13 @@ def main():
             "host_roundtrip_GiBps": rt,
             "host_roundtrip_ranks": world if rt is not None else None,
             "host_roundtrip_parity": rt_ok,
-            "parity_spot_check": parity,
+            "parity": parity,
+            "parity_spot_check": bool(parity and parity["all_blocks_match"]),
             "digests": [hex(d) for d in digests],
         }
         print(json.dumps(line), flush=True)
     ctx.close()
-    if world > 1:
+    if dd:
         dist.destroy_process_group()
 
 

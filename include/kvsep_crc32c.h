@@ -156,6 +156,47 @@ int kvsep_sst_verify_device(kvsep_crc32c_ctx* ctx, void* stream, const void* fil
                             const uint64_t* len, uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count,
                             uint64_t total_bytes, uint64_t max_len);
 
+/* ---------------------------------------------------------------- several GPUs in one process
+ * Blocks are independent, so a batch is cut into contiguous block ranges balanced by bytes and each range runs on
+ * its own device; payload never crosses between GPUs, only the u32 results come back (into ONE array).  For a
+ * single KVDB process scanning whole vlogs (GC db/db_impl.cc:880-951, recovery :485-571) on every GPU it has. */
+/* bounds[0..parts]: part p = blocks [bounds[p], bounds[p+1]), each ~sum(len)/parts bytes (the cut nearest to each
+ * p/parts point of the prefix sum of len).  Host arrays; no device needed. */
+int kvsep_crc32c_partition(const uint64_t* len, uint64_t count, int parts, uint64_t* bounds);
+typedef struct kvsep_crc32c_group kvsep_crc32c_group;
+/* One context (and stream) per listed device; a device may be listed twice (two independent contexts on it). */
+int kvsep_crc32c_group_create(const int* devices, int ndev, kvsep_crc32c_group** out);
+void kvsep_crc32c_group_destroy(kvsep_crc32c_group* g);
+int kvsep_crc32c_group_size(kvsep_crc32c_group* g);
+kvsep_crc32c_ctx* kvsep_crc32c_group_ctx(kvsep_crc32c_group* g, int i); /* member i's context (tuning knobs) */
+/* kvsep_crc32c_batch_host_span over the whole group: part i through member i's pinned staging on its own PCIe link,
+ * one host thread per member; blocking. */
+int kvsep_crc32c_group_batch_host_span(kvsep_crc32c_group* g, const char* host_base, uint64_t span_bytes,
+                                       const uint64_t* off, const uint64_t* len, const uint32_t* init, uint32_t* out,
+                                       uint64_t count);
+/* ... plus Mask(out[i]) == expected_masked[i]: *first_bad = lowest mismatching index (UINT64_MAX if none), *nbad. */
+int kvsep_crc32c_group_verify_host_span(kvsep_crc32c_group* g, const char* host_base, uint64_t span_bytes,
+                                        const uint64_t* off, const uint64_t* len, const uint32_t* init,
+                                        const uint32_t* expected_masked, uint32_t* out, uint64_t* first_bad,
+                                        uint64_t* nbad, uint64_t count);
+/* kvsep_vlog_verify_host with the checksums spread over the group. */
+int kvsep_vlog_verify_host_group(kvsep_crc32c_group* g, const char* buf, uint64_t n, uint64_t* nrecords,
+                                 uint64_t* ngood, uint64_t* good_bytes, uint64_t* drop_bytes);
+/* Device-resident shards: member i's blocks live on ITS device (base[i], off[i], len[i], init[i] (nullable array or
+ * entries), out[i] are device pointers there, count[i] blocks, total_bytes[i] / max_len[i] hints as in
+ * kvsep_crc32c_batch_device).  Runs every shard on its member's stream and returns when all are done. */
+int kvsep_crc32c_group_batch_device(kvsep_crc32c_group* g, const void* const* base, const uint64_t* const* off,
+                                    const uint64_t* const* len, const uint32_t* const* init, uint32_t* const* out,
+                                    const uint64_t* count, const uint64_t* total_bytes, const uint64_t* max_len);
+/* ... verify form: shard i's block k is global block index_base[i] + k; *first_bad = the lowest global mismatching
+ * index over all shards (UINT64_MAX if none), *nbad = the total -- the reduction SURVEY §8e puts on RCCL between
+ * ranks, done here between the members of one process.  expected_masked may be NULL (then = batch_device). */
+int kvsep_crc32c_group_verify_device(kvsep_crc32c_group* g, const void* const* base, const uint64_t* const* off,
+                                     const uint64_t* const* len, const uint32_t* const* init,
+                                     const uint32_t* const* expected_masked, uint32_t* const* out,
+                                     const uint64_t* index_base, const uint64_t* count, const uint64_t* total_bytes,
+                                     const uint64_t* max_len, uint64_t* first_bad, uint64_t* nbad);
+
 /* Pinned (page-locked) host memory for file images: read a vlog / SST file straight into it and the
  * host-span entry points DMA from it directly, without the staging memcpy.  NULL on failure. */
 void* kvsep_host_alloc_pinned(uint64_t bytes);

@@ -98,6 +98,22 @@ _SIGS = {
     "kvsep_sst_verify_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]),
+    "kvsep_crc32c_partition": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]),
+    "kvsep_crc32c_group_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "kvsep_crc32c_group_destroy": (None, [ctypes.c_void_p]),
+    "kvsep_crc32c_group_size": (ctypes.c_int, [ctypes.c_void_p]),
+    "kvsep_crc32c_group_ctx": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_int]),
+    "kvsep_crc32c_group_batch_host_span": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                          ctypes.c_void_p, ctypes.c_uint64]),
+    "kvsep_crc32c_group_verify_host_span": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                           ctypes.c_void_p, ctypes.c_uint64]),
+    "kvsep_vlog_verify_host_group": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "kvsep_crc32c_group_batch_device": (ctypes.c_int, [ctypes.c_void_p] * 10),
+    "kvsep_crc32c_group_verify_device": (ctypes.c_int, [ctypes.c_void_p] * 14),
     "kvsep_host_alloc_pinned": (ctypes.c_void_p, [ctypes.c_uint64]),
     "kvsep_host_free_pinned": (None, [ctypes.c_void_p]),
     "kvsep_last_error": (ctypes.c_char_p, []),
@@ -442,6 +458,97 @@ def log_accept(off, ok, n: int):
     dropped = lib().kvsep_log_accept(off.ctypes.data_as(ctypes.c_void_p), ok.ctypes.data_as(ctypes.c_void_p),
                                      off.size, n, acc.ctypes.data_as(ctypes.c_void_p))
     return acc[:off.size], int(dropped)
+
+
+def partition(length, parts: int) -> np.ndarray:
+    """kvsep_crc32c_partition: block-range bounds (parts + 1 entries) balanced by bytes."""
+    length = np.ascontiguousarray(length, dtype=np.uint64)
+    b = np.zeros(parts + 1, dtype=np.uint64)
+    _check(lib().kvsep_crc32c_partition(length.ctypes.data_as(ctypes.c_void_p), length.size, parts,
+                                        b.ctypes.data_as(ctypes.c_void_p)), "kvsep_crc32c_partition")
+    return b
+
+
+class Group:
+    """Several devices in one process (kvsep_crc32c_group_*): one context and stream per listed device."""
+
+    def __init__(self, devices):
+        arr = (ctypes.c_int * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        _check(lib().kvsep_crc32c_group_create(arr, len(devices), ctypes.byref(h)), "kvsep_crc32c_group_create")
+        self._h = h
+        self.devices = list(devices)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().kvsep_crc32c_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def size(self) -> int:
+        return lib().kvsep_crc32c_group_size(self._h)
+
+    def batch_host_span(self, buf, off, length, init=None, expected_masked=None):
+        """-> out, or (out, first_bad, nbad) with expected_masked."""
+        p, keep = _buf(buf)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint64)
+        out = np.zeros(off.size, dtype=np.uint32)
+        vp = ctypes.c_void_p
+        ip = None if init is None else np.ascontiguousarray(init, dtype=np.uint32)
+        ipp = None if ip is None else ip.ctypes.data_as(vp)
+        if expected_masked is None:
+            _check(lib().kvsep_crc32c_group_batch_host_span(self._h, p, keep.nbytes, off.ctypes.data_as(vp),
+                                                            length.ctypes.data_as(vp), ipp, out.ctypes.data_as(vp),
+                                                            off.size), "kvsep_crc32c_group_batch_host_span")
+            return out
+        ex = np.ascontiguousarray(expected_masked, dtype=np.uint32)
+        fb, nb = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().kvsep_crc32c_group_verify_host_span(self._h, p, keep.nbytes, off.ctypes.data_as(vp),
+                                                         length.ctypes.data_as(vp), ipp, ex.ctypes.data_as(vp),
+                                                         out.ctypes.data_as(vp), ctypes.byref(fb), ctypes.byref(nb),
+                                                         off.size), "kvsep_crc32c_group_verify_host_span")
+        return out, fb.value, nb.value
+
+    def vlog_verify(self, image):
+        """kvsep_vlog_verify_host_group -> (records, good, good_bytes, drop_bytes)."""
+        p, keep = _buf(image)
+        v = [ctypes.c_uint64() for _ in range(4)]
+        _check(lib().kvsep_vlog_verify_host_group(self._h, p, keep.nbytes, *[ctypes.byref(x) for x in v]),
+               "kvsep_vlog_verify_host_group")
+        return tuple(x.value for x in v)
+
+    def batch_device(self, shards, expected_masked=None, index_base=None):
+        """shards: per member a dict(base=, off=, len=, out=, [init=], total_bytes=, max_len=) of device tensors /
+        addresses on that member's device.  -> None, or (first_bad, nbad) over all shards with expected_masked
+        (per-member device arrays) and index_base (global index of each shard's first block)."""
+        n = len(shards)
+        P = ctypes.c_void_p * n
+        U = ctypes.c_uint64 * n
+        base = P(*[_dptr(s["base"]).value for s in shards])
+        off = P(*[_dptr(s["off"]).value for s in shards])
+        ln = P(*[_dptr(s["len"]).value for s in shards])
+        out = P(*[_dptr(s["out"]).value for s in shards])
+        init = P(*[_dptr(s.get("init")).value for s in shards])
+        cnt = U(*[int(s["off"].numel()) for s in shards])
+        tot = U(*[int(s["total_bytes"]) for s in shards])
+        ml = U(*[int(s.get("max_len", 0)) for s in shards])
+        if expected_masked is None:
+            _check(lib().kvsep_crc32c_group_batch_device(self._h, base, off, ln, init, out, cnt, tot, ml),
+                   "kvsep_crc32c_group_batch_device")
+            return None
+        ex = P(*[_dptr(e).value for e in expected_masked])
+        ib = U(*[int(x) for x in index_base])
+        fb, nb = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().kvsep_crc32c_group_verify_device(self._h, base, off, ln, init, ex, out, ib, cnt, tot, ml,
+                                                      ctypes.byref(fb), ctypes.byref(nb)),
+               "kvsep_crc32c_group_verify_device")
+        return fb.value, nb.value
 
 
 def fill_splitmix64(dst, nbytes: int, seed: int, stream_offset: int = 0, stream=None):

@@ -1,9 +1,12 @@
-"""Multi-GPU sharding of a CRC batch: blocks are independent, so each rank checksums
-its own shard from its own HBM and only 8-byte digests / timings cross the interconnect.
+"""Multi-GPU sharding of a CRC batch: blocks are independent, so each rank checksums its own
+shard from its own HBM; only the u32 results (4 B per block), verify counts and timings cross the interconnect.
 
-Weak scaling: every rank holds the same block layout over its own slice of one global splitmix64
-stream -- rank r's byte j is global stream byte r*span + j -- so the N-GPU job equals one logical
-batch of N*count blocks.  Used by bench.py on RCCL and by tests/test_multiprocess_cpu.py on gloo.
+Two ways a batch is spread over ranks, both one logical batch of the whole job:
+  * uniform configs (2, 3a, 3b): every rank holds the same block layout over its own slice of one global
+    splitmix64 stream -- rank r's byte j is global stream byte r*span + j (weak scaling);
+  * ragged config 4: one global batch of world x 2^20 Zipf blocks, cut into contiguous block ranges balanced by
+    bytes (kvsep_crc32c_partition, a prefix sum of len), one range per rank.
+Used by bench.py on RCCL and by tests/test_multiprocess_cpu.py on gloo.
 """
 from __future__ import annotations
 
@@ -21,6 +24,44 @@ def global_layout(off: np.ndarray, length: np.ndarray, span: int, world: int):
     length = np.asarray(length, dtype=np.uint64)
     offs = np.concatenate([off + np.uint64(stream_offset(r, span)) for r in range(world)])
     return offs, np.tile(length, world)
+
+
+def partition_layout(goff: np.ndarray, glen: np.ndarray, world: int, rank: int):
+    """Rank `rank`'s part of one global batch (global offsets goff into one stream, lengths glen), balanced by bytes:
+    -> (local offsets from the part's first byte, lengths, stream base = global byte offset of that first byte,
+    index base = global index of the part's first block)."""
+    from kvsep import partition
+
+    b = partition(glen, world)
+    b0, b1 = int(b[rank]), int(b[rank + 1])
+    goff = np.asarray(goff, dtype=np.uint64)
+    glen = np.asarray(glen, dtype=np.uint64)
+    if b1 == b0:
+        return np.zeros(0, np.uint64), np.zeros(0, np.uint64), 0, b0
+    base = int(goff[b0])
+    return goff[b0:b1] - np.uint64(base), glen[b0:b1].copy(), base, b0
+
+
+def gather_results(crcs: np.ndarray, dist, device) -> list[np.ndarray]:
+    """All-gather every rank's u32 results (any lengths) -> the list of per-rank arrays on every rank: the result
+    traffic of SURVEY.md §8e, 4 B per block (2 MiB for config 5's 524,288 records)."""
+    import torch
+
+    crcs = np.ascontiguousarray(crcs, dtype=np.uint32)
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return [crcs]
+    world = dist.get_world_size()
+    n = torch.tensor([crcs.size], dtype=torch.int64, device=device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    ns = [int(x.item()) for x in ns]
+    m = max(ns)
+    t = torch.zeros(m, dtype=torch.int32, device=device)
+    if crcs.size:
+        t[:crcs.size] = torch.from_numpy(crcs.view(np.int32)).to(device)
+    outs = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(outs, t)
+    return [o[:k].cpu().numpy().view(np.uint32).copy() for o, k in zip(outs, ns)]
 
 
 def crc_of_crcs(crcs: np.ndarray, extend_host) -> int:

@@ -101,3 +101,22 @@ def test_ctx_without_gpu_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(kvsep.KvsepError):
         kvsep.Context(0)
+
+
+def test_partition_byte_balanced():
+    """kvsep_crc32c_partition: contiguous, monotone, covers every block, each part within one
+    block of its byte share; degenerate inputs."""
+    from kvsep import workloads as W
+
+    for count, parts in ((1 << 20, 8), (1000, 3), (5, 8), (1, 1), (0, 4)):
+        ln = W.zipf_lengths(count) if count else np.zeros(0, np.uint64)
+        b = kvsep.partition(ln, parts)
+        assert b[0] == 0 and b[-1] == count and np.all(np.diff(b.astype(np.int64)) >= 0)
+        if count:
+            pre = np.concatenate([[0], np.cumsum(ln, dtype=np.uint64)])
+            share = pre[-1] / parts
+            for p in range(parts):
+                got = int(pre[b[p + 1]] - pre[b[p]])
+                assert abs(got - share) <= int(ln.max()), (count, parts, p, got, share)
+    b = kvsep.partition(np.array([10, 0, 0, 10], np.uint64), 2)
+    assert b.tolist() in ([0, 1, 4], [0, 2, 4], [0, 3, 4])

@@ -83,3 +83,69 @@ def test_two_rank_shards_equal_one_logical_batch(oracle):
     assert np.array_equal(got, exp)
     assert res[0][1] == [shard.crc_of_crcs(exp[:COUNT], kvsep.extend_host),
                          shard.crc_of_crcs(exp[COUNT:], kvsep.extend_host)]
+
+
+RAGGED_COUNT, RAGGED_CAP, RAGGED_SEED = 3000, 50_000, 0x5EED4
+
+
+def _ragged_layout():
+    sys.path.insert(0, os.path.join(ROOT, "kv-separate_amd"))
+    from kvsep import workloads as W
+
+    glen = np.minimum(W.zipf_lengths(RAGGED_COUNT), RAGGED_CAP).astype(np.uint64)  # config-4 shape, capped for CPU
+    goff = np.zeros(RAGGED_COUNT, np.uint64)
+    goff[1:] = np.cumsum(glen[:-1], dtype=np.uint64)
+    return goff, glen
+
+
+def _ragged_worker(rank, world, port, q):
+    sys.path.insert(0, os.path.join(ROOT, "kv-separate_amd"))
+    import kvsep
+    from kvsep import shard, splitmix64_bytes
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cpu")
+    goff, glen = _ragged_layout()
+    off, ln, base, ib = shard.partition_layout(goff, glen, world, rank)  # bench.py's config-4 split
+    span = int(off[-1] + ln[-1]) if ln.size else 0
+    data = splitmix64_bytes(span + 16, RAGGED_SEED, base)
+    crcs = np.array([kvsep.extend_host(0, data[int(o):int(o + l)]) for o, l in zip(off, ln)], dtype=np.uint32)
+    parts = shard.gather_results(crcs, dist, dev)
+    stored = np.array([kvsep.mask(int(c)) for c in crcs], np.uint32)
+    if rank == world - 1:
+        stored[5] ^= 0x40
+    bad = np.flatnonzero(np.array([kvsep.mask(int(c)) for c in crcs], np.uint32) != stored)
+    nbad, first = shard.reduce_verify(int(bad.size), ib + int(bad[0]) if bad.size else -1, dist, dev)
+    q.put((rank, [p.tolist() for p in parts], ib, int(ln.sum()), nbad, first))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ragged_batch_byte_balanced_over_ranks(oracle, world):
+    """Config-4-shaped ragged lengths split over gloo ranks by kvsep_crc32c_partition (byte-balanced contiguous
+    block ranges), u32 results all-gathered, verify counts reduced: one logical batch, checked by the oracle."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ragged_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from kvsep import splitmix64_bytes
+
+    goff, glen = _ragged_layout()
+    exp = oracle.batch(splitmix64_bytes(int(glen.sum()) + 16, RAGGED_SEED, 0), goff, glen, threads=4)
+    for r in range(world):
+        got = np.concatenate([np.array(p, np.uint32) for p in res[r][1]])
+        assert np.array_equal(got, exp)  # every rank holds the whole result vector
+    total = int(glen.sum())
+    assert [x[2] for x in res] == sorted(x[2] for x in res) and res[0][2] == 0
+    for r in range(world):  # byte balance: within one block of the even share
+        assert abs(res[r][3] - total / world) <= int(glen.max())
+    last_ib = res[-1][2]
+    assert all(x[4] == 1 and x[5] == last_ib + 5 for x in res)
