@@ -112,8 +112,8 @@ _SIGS = {
                                                            ctypes.c_void_p, ctypes.c_uint64]),
     "kvsep_vlog_verify_host_group": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
-    "kvsep_crc32c_group_batch_device": (ctypes.c_int, [ctypes.c_void_p] * 10),
-    "kvsep_crc32c_group_verify_device": (ctypes.c_int, [ctypes.c_void_p] * 14),
+    "kvsep_crc32c_group_batch_device": (ctypes.c_int, [ctypes.c_void_p] * 9),
+    "kvsep_crc32c_group_verify_device": (ctypes.c_int, [ctypes.c_void_p] * 13),
     "kvsep_host_alloc_pinned": (ctypes.c_void_p, [ctypes.c_uint64]),
     "kvsep_host_free_pinned": (None, [ctypes.c_void_p]),
     "kvsep_last_error": (ctypes.c_char_p, []),
