@@ -731,7 +731,7 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
 }
 
 // Unsplit batches only (every block <= 64 KiB <= piece_bytes); static contiguous runs of 8-block groups.
-template <int kG, bool kNT, int kThreads, bool kOverlap = false>
+template <int kG, bool kNT, int kThreads, bool kOverlap = false, int kPrio = 0, int kSkew = 0>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -750,8 +750,20 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   // fewer groups than waves the busy waves are spread over every CU instead of filling the first CUs.
   const uint64_t groups = (a.count + kPerGroup - 1) / kPerGroup;
   const uint64_t gper = (groups + nwaves - 1) / nwaves;
-  const uint64_t lo = (uint64_t(wave) * gridDim.x + blockIdx.x) * gper * kPerGroup;
+  uint64_t lo = (uint64_t(wave) * gridDim.x + blockIdx.x) * gper * kPerGroup;
   uint64_t hi = lo + gper * kPerGroup;
+  if (kSkew && kWavesPerWg == 16) {
+    // KVSEP_DIAG experiment: the workgroup's contiguous run split over its waves by issue rank (wave w is the
+    // (w >> 2)-th wave on its SIMD); later-ranked waves get fewer blocks (72:68:60:56 per rank)
+    const uint64_t per_wg = (a.count + gridDim.x - 1) / gridDim.x;
+    const uint64_t b0 = uint64_t(blockIdx.x) * per_wg;
+    const uint64_t L = b0 < a.count ? (b0 + per_wg < a.count ? per_wg : a.count - b0) : 0;
+    constexpr uint32_t cw[5] = {0, 72, 140, 200, 256};
+    const uint32_t q = wave >> 2, r = wave & 3;
+    const uint64_t s0 = 4 * cw[q] + r * (cw[q + 1] - cw[q]), s1 = s0 + (cw[q + 1] - cw[q]);
+    lo = b0 + L * s0 / 1024;
+    hi = b0 + L * s1 / 1024;
+  }
   if (hi > a.count) hi = a.count;
 
   // Descriptors run one group ahead of the staging: taking group g stages its rows from descriptors loaded
@@ -803,8 +815,16 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     it.kmax = km;
     it.kmin = kn;
   };
+  uint32_t done = 0;  // groups finished by this wave (kPrio: waves that are ahead yield issue slots)
   auto step = [&](uint64_t g, NItem& ia, NStaged<kG>& A, NItem& ib, NStaged<kG>& B) {
     const uint64_t gn = g + kPerGroup;
+    if (kPrio) {
+      if (done == 0) __builtin_amdgcn_s_setprio(3);
+      else if (done == 1) __builtin_amdgcn_s_setprio(2);
+      else if (done == 2) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+      ++done;
+    }
     // the next group is staged inside nfinish, after this group's last row loads; unconditional (past the
     // end it is an empty group of dummy loads: see the wide kernel's step())
     const uint32_t reg = nfinish<kG, kNT>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
@@ -816,6 +836,21 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
 
   NItem cur, nxt;
   NStaged<kG> S, T;
+#ifdef KVSEP_STAMPS  // diagnostic build (tools/stamp_probe.hip): realtime (100 MHz) at entry, after the fill, after
+                     // each group (up to 5), and at exit, per wave
+  unsigned long long* nst = &g_kvsep_stamps[(uint64_t(blockIdx.x) * kWavesPerWg + wave) * 8];
+  unsigned long long tnow;
+  int nsteps = 0;
+  KVSEP_RSTAMP(tnow);
+  if (lane == 0) nst[0] = tnow;
+#define KVSEP_NSTAMP(k)                  \
+  do {                                   \
+    KVSEP_RSTAMP(tnow);                  \
+    if (lane == 0) nst[k] = tnow;        \
+  } while (0)
+#else
+#define KVSEP_NSTAMP(k) do {} while (0)
+#endif
   // The first group's descriptors are fetched during the LDS fill.  Staging its rows before the fill as well
   // measured 4-7 % slower on 256 MiB-1 GiB batches of 4 KiB blocks: the fill then waits behind them.
   if (kOverlap) {
@@ -837,12 +872,25 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
       load_desc(lo + kPerGroup, dn);
     }
   }
+  KVSEP_NSTAMP(1);
+#ifdef KVSEP_STAMPS
+#define KVSEP_NSTEP() do { if (nsteps < 5) KVSEP_NSTAMP(2 + nsteps); ++nsteps; } while (0)
+#else
+#define KVSEP_NSTEP() do {} while (0)
+#endif
   if (lo < hi) {
     for (uint64_t g = lo;; g += 2 * kPerGroup) {
-      if (!step(g, cur, S, nxt, T)) break;
-      if (!step(g + kPerGroup, nxt, T, cur, S)) break;
+      const bool more = step(g, cur, S, nxt, T);
+      KVSEP_NSTEP();
+      if (!more) break;
+      const bool more2 = step(g + kPerGroup, nxt, T, cur, S);
+      KVSEP_NSTEP();
+      if (!more2) break;
     }
   }
+  KVSEP_NSTAMP(7);
+#undef KVSEP_NSTEP
+#undef KVSEP_NSTAMP
   if (deferred) {
     // Blocks longer than the hint: the wave walks its run again and checksums those blocks one at a time, each
     // cut into 8 contiguous sub-ranges, one per slot (full 64-bit length), merged with R(A||B) = Z_|B|(R(A)) ^ R(B)
@@ -1320,6 +1368,11 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
       case 3: crc32c_narrow_kernel<4, true, 768><<<grid, 768, 0, s>>>(a); break;
       case 4: crc32c_narrow_kernel<8, true, 512><<<grid, 512, 0, s>>>(a); break;
       case 5: crc32c_narrow_kernel<8, true, 768><<<grid, 768, 0, s>>>(a); break;
+      case 10: crc32c_narrow_kernel<4, true, 1024, false, 1><<<grid, 1024, 0, s>>>(a); break;
+      case 11: crc32c_narrow_kernel<4, true, 512, true, 1><<<grid, 512, 0, s>>>(a); break;
+      case 12: crc32c_narrow_kernel<8, true, 512, true><<<grid, 512, 0, s>>>(a); break;
+      case 13: crc32c_narrow_kernel<4, true, 1024, false, 0, 1><<<grid, 1024, 0, s>>>(a); break;
+      case 14: crc32c_narrow_kernel<4, true, 1024, true><<<grid, 1024, 0, s>>>(a); break;
 #endif
       case 9: crc32c_narrow_kernel<4, true, 512, true><<<grid, 512, 0, s>>>(a); break;
       default: crc32c_narrow_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
