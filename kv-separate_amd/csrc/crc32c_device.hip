@@ -385,14 +385,24 @@ struct NoMid {
 
 // `mid()` runs between the fill's global loads and its LDS stores (pinned there by sched barriers): loads it
 // issues are younger than the table loads, so the stores wait for the tables only (a counted vmcnt).
-template <int kThreads = kWgThreads, typename Mid = NoMid>
+// kNarrowSet: only the small tables the narrow kernel reads -- Z_4, Z_16, Z_32, Z_64 (one 16 KiB run from kZ4Off)
+// and the byte table -- not Z_128 .. Z_512 (12 KiB less to load and store per workgroup).
+constexpr uint32_t kSmallAll16 = (kLdsBytes - kZ4Off) / 16;                       // uint4 in the small-table run
+constexpr uint32_t kSmallNarrow16 = (4 * 4096) / 16 + 1024 / 16;                  // Z_4..Z_64 + byte table
+template <bool kNarrowSet>
+__device__ __forceinline__ uint32_t small_index(uint32_t q) {  // uint4 index from kZ4Off (same in src and LDS)
+  return !kNarrowSet || q < 1024 ? q : (kByteOff - kZ4Off) / 16 + (q - 1024);
+}
+
+template <int kThreads = kWgThreads, bool kNarrowSet = false, typename Mid = NoMid>
 __device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* rep, const DevTables* tabs, uint32_t tid,
                                          Mid&& mid = Mid()) {
   // Every global load of the fill is issued before the first LDS store: one L2/HBM round trip per
   // workgroup instead of one per loop trip (the fill is a fixed cost of every launch; it dominates
   // small batches, e.g. 4 KiB-block batches of a few MiB).
   constexpr uint32_t kRep = (8192 + kThreads - 1) / kThreads;                           // uint4 stores
-  constexpr uint32_t kSmall = ((kLdsBytes - kZ4Off) / 16 + kThreads - 1) / kThreads;  // uint4 copies
+  constexpr uint32_t kN16 = kNarrowSet ? kSmallNarrow16 : kSmallAll16;
+  constexpr uint32_t kSmall = (kN16 + kThreads - 1) / kThreads;                        // uint4 copies
   uint4* l128 = reinterpret_cast<uint4*>(lds);
   const uint4* src = reinterpret_cast<const uint4*>(&tabs->z4[0][0]);
   uint32_t v[kRep];
@@ -406,7 +416,7 @@ __device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* rep, cons
 #pragma unroll
   for (uint32_t i = 0; i < kSmall; ++i) {
     const uint32_t q = tid + i * kThreads;
-    w[i] = q < (kLdsBytes - kZ4Off) / 16 ? src[q] : make_uint4(0, 0, 0, 0);
+    w[i] = q < kN16 ? src[small_index<kNarrowSet>(q)] : make_uint4(0, 0, 0, 0);
   }
   __builtin_amdgcn_sched_barrier(0);
   mid();
@@ -420,7 +430,7 @@ __device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* rep, cons
 #pragma unroll
   for (uint32_t i = 0; i < kSmall; ++i) {
     const uint32_t q = tid + i * kThreads;
-    if (q < (kLdsBytes - kZ4Off) / 16) l128[kZ4Off / 16 + q] = w[i];
+    if (q < kN16) l128[kZ4Off / 16 + small_index<kNarrowSet>(q)] = w[i];
   }
 }
 
@@ -858,14 +868,14 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     // only, so the first HBM round trip overlaps the fill.  Unconditional (an idle wave stages an empty
     // group), so the store's wait count is the same on every path.
     load_desc(lo, dn);
-    fill_lds<kThreads>(lds, &a.tabs->znarrow[0][0], a.tabs, tid, [&]() {
+    fill_lds<kThreads, true>(lds, &a.tabs->znarrow[0][0], a.tabs, tid, [&]() {
       take(lo, cur, S);
       load_desc(lo + kPerGroup, dn);
     });
     __syncthreads();
   } else {
     if (lo < hi) load_desc(lo, dn);
-    fill_lds<kThreads>(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
+    fill_lds<kThreads, true>(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
     __syncthreads();
     if (lo < hi) {
       take(lo, cur, S);

@@ -7,7 +7,8 @@ O=$R/gpurun_out
 D=$R/profiles/${1:?round name}
 mkdir -p $D
 cp $O/bench_default.json $D/bench_default.json
-for c in 3b 4 2; do cp $O/bench_cfg$c.json $D/bench_cfg$c.json; done
+for c in 3b 4 2 5; do cp $O/bench_cfg$c.json $D/bench_cfg$c.json; done
+cp $O/launch_floor.txt $D/launch_floor.txt
 cp $O/framing_bench.json $D/framing_bench.json
 cp $O/prof/stats_kernel_stats.csv $D/kernel_stats_cfg3a.csv
 cp $O/prof/stats_kernel_trace.csv $D/kernel_trace_cfg3a.csv

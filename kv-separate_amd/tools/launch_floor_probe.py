@@ -63,7 +63,7 @@ for mib in sizes:
     ideal = total / 8e12 * 1e6
     for name, fn in rows:
         mn, med = graph_avg_us(fn)
-        print(f"{mib:5d} MiB {name:42s} min {mn:8.2f} us  med {med:8.2f} us  {total / med / 1e6:8.1f} GB/s  "
+        print(f"{mib:5d} MiB {name:42s} min {mn:8.2f} us  med {med:8.2f} us  {total / med / 1e6:6.2f} TB/s  "
               f"(8 TB/s: {ideal:7.2f} us)", flush=True)
     del data, d_off, d_len, out
     torch.cuda.empty_cache()

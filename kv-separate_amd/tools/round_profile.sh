@@ -7,9 +7,10 @@ mkdir -p $O
 cd $R
 timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err || exit 1
 timeout -k 10 400 python -u kv-separate_amd/tools/framing_bench.py --out $O/framing_bench.json > $O/framing_bench.log 2>&1 || exit 1
-for c in 3b 4 2; do
+for c in 3b 4 2 5; do
   timeout -k 10 400 python bench.py --config $c --steps 10 --warmup 2 --no-cpu --roundtrip-gib 0 > $O/bench_cfg$c.json 2>$O/bench_cfg$c.err || exit 1
 done
+timeout -k 10 300 python -u kv-separate_amd/tools/launch_floor_probe.py 64 256 1024 4096 > $O/launch_floor.txt 2>&1 || exit 1
 export TMPDIR=/tmp
 cd /tmp
 B="$R/bench.py --steps 3 --warmup 1 --no-cpu --roundtrip-gib 0"
