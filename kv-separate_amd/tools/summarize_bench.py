@@ -11,5 +11,5 @@ for f in sorted(sys.argv[1:]):
         continue
     r = d["roofline"]
     print(f"{f:40s} {d['value']:9.1f} GiB/s {d['ms_per_step']:8.3f} ms  kern {r['achieved']:7.1f} GB/s "
-          f"frac {r['frac']:.4f} ceil {d['read_ceiling_GBps']:7.1f} ({d['frac_of_read_ceiling']:.3f}) "
-          f"par {d['parity_spot_check']} rt {d['host_roundtrip_GiBps']} cpu {(d['cpu_baseline'] or {}).get('value')}")
+          f"frac {r['frac']:.4f} ceil {d['read_ceiling_GBps']} ({d['frac_of_read_ceiling']}) "
+          f"par {d.get('parity') or d['parity_spot_check']} rt {d['host_roundtrip_GiBps']} cpu {(d['cpu_baseline'] or {}).get('value')}")
