@@ -741,7 +741,7 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
 }
 
 // Unsplit batches only (every block <= 64 KiB <= piece_bytes); static contiguous runs of 8-block groups.
-template <int kG, bool kNT, int kThreads, bool kOverlap = false, int kPrio = 0, int kSkew = 0>
+template <int kG, bool kNT, int kThreads, bool kOverlap = false>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -760,20 +760,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   // fewer groups than waves the busy waves are spread over every CU instead of filling the first CUs.
   const uint64_t groups = (a.count + kPerGroup - 1) / kPerGroup;
   const uint64_t gper = (groups + nwaves - 1) / nwaves;
-  uint64_t lo = (uint64_t(wave) * gridDim.x + blockIdx.x) * gper * kPerGroup;
+  const uint64_t lo = (uint64_t(wave) * gridDim.x + blockIdx.x) * gper * kPerGroup;
   uint64_t hi = lo + gper * kPerGroup;
-  if (kSkew && kWavesPerWg == 16) {
-    // KVSEP_DIAG experiment: the workgroup's contiguous run split over its waves by issue rank (wave w is the
-    // (w >> 2)-th wave on its SIMD); later-ranked waves get fewer blocks (72:68:60:56 per rank)
-    const uint64_t per_wg = (a.count + gridDim.x - 1) / gridDim.x;
-    const uint64_t b0 = uint64_t(blockIdx.x) * per_wg;
-    const uint64_t L = b0 < a.count ? (b0 + per_wg < a.count ? per_wg : a.count - b0) : 0;
-    constexpr uint32_t cw[5] = {0, 72, 140, 200, 256};
-    const uint32_t q = wave >> 2, r = wave & 3;
-    const uint64_t s0 = 4 * cw[q] + r * (cw[q + 1] - cw[q]), s1 = s0 + (cw[q + 1] - cw[q]);
-    lo = b0 + L * s0 / 1024;
-    hi = b0 + L * s1 / 1024;
-  }
   if (hi > a.count) hi = a.count;
 
   // Descriptors run one group ahead of the staging: taking group g stages its rows from descriptors loaded
@@ -825,16 +813,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     it.kmax = km;
     it.kmin = kn;
   };
-  uint32_t done = 0;  // groups finished by this wave (kPrio: waves that are ahead yield issue slots)
   auto step = [&](uint64_t g, NItem& ia, NStaged<kG>& A, NItem& ib, NStaged<kG>& B) {
     const uint64_t gn = g + kPerGroup;
-    if (kPrio) {
-      if (done == 0) __builtin_amdgcn_s_setprio(3);
-      else if (done == 1) __builtin_amdgcn_s_setprio(2);
-      else if (done == 2) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
-      ++done;
-    }
     // the next group is staged inside nfinish, after this group's last row loads; unconditional (past the
     // end it is an empty group of dummy loads: see the wide kernel's step())
     const uint32_t reg = nfinish<kG, kNT>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
@@ -1378,10 +1358,7 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
       case 3: crc32c_narrow_kernel<4, true, 768><<<grid, 768, 0, s>>>(a); break;
       case 4: crc32c_narrow_kernel<8, true, 512><<<grid, 512, 0, s>>>(a); break;
       case 5: crc32c_narrow_kernel<8, true, 768><<<grid, 768, 0, s>>>(a); break;
-      case 10: crc32c_narrow_kernel<4, true, 1024, false, 1><<<grid, 1024, 0, s>>>(a); break;
-      case 11: crc32c_narrow_kernel<4, true, 512, true, 1><<<grid, 512, 0, s>>>(a); break;
       case 12: crc32c_narrow_kernel<8, true, 512, true><<<grid, 512, 0, s>>>(a); break;
-      case 13: crc32c_narrow_kernel<4, true, 1024, false, 0, 1><<<grid, 1024, 0, s>>>(a); break;
       case 14: crc32c_narrow_kernel<4, true, 1024, true><<<grid, 1024, 0, s>>>(a); break;
 #endif
       case 9: crc32c_narrow_kernel<4, true, 512, true><<<grid, 512, 0, s>>>(a); break;
