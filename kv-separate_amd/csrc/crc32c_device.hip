@@ -666,7 +666,7 @@ __device__ __forceinline__ void nstage(NStaged<kG>& s, uintptr_t ps, uintptr_t p
 
 // Raw register after the slot item, valid in the slot's last lane (j == 7).  kmin / kmax: wave min / max of K.
 // `next()` stages the following group, after this group's last row loads (see the wide kernel's finish()).
-template <int kG, bool kNT, typename Next>
+template <int kG, bool kNT, int kAbl = 0, typename Next>  // kAbl != 0: KVSEP_DIAG ablation (wrong results)
 __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, uint32_t reg, uint32_t j,
                                             uint32_t lc0, uint32_t lc1, uint32_t kmin, uint32_t kmax,
                                             uintptr_t dummy, Next&& next) {
@@ -682,12 +682,16 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
     uint4 v = (K && s.seg >= h0) ? s.v : make_uint4(0, 0, 0, 0);
     if (K && s.seg == h0) v.x ^= reg;  // the head register enters as pending word at h0
     uint32_t c0 = v.x, c1 = v.y, c2 = v.z, c3 = v.w;
-#define KVSEP_NROW(V)                          \
-  do {                                         \
-    c0 = fold_step(lds, c0, (V).x, lc0, lc1);  \
-    c1 = fold_step(lds, c1, (V).y, lc0, lc1);  \
-    c2 = fold_step(lds, c2, (V).z, lc0, lc1);  \
-    c3 = fold_step(lds, c3, (V).w, lc0, lc1);  \
+#define KVSEP_NROW(V)                                                 \
+  do {                                                                \
+    if (kAbl) {                                                       \
+      c0 ^= (V).x; c1 ^= (V).y; c2 ^= (V).z; c3 ^= (V).w;             \
+    } else {                                                          \
+      c0 = fold_step(lds, c0, (V).x, lc0, lc1);                       \
+      c1 = fold_step(lds, c1, (V).y, lc0, lc1);                       \
+      c2 = fold_step(lds, c2, (V).z, lc0, lc1);                       \
+      c3 = fold_step(lds, c3, (V).w, lc0, lc1);                       \
+    }                                                                 \
   } while (0)
     uint32_t r = 1;
     for (; r + 2 * kG <= kmin; r += kG) {  // every slot has rows r .. r+2kG-1: no guards, no clamps
@@ -741,7 +745,7 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
 }
 
 // Unsplit batches only (every block <= 64 KiB <= piece_bytes); static contiguous runs of 8-block groups.
-template <int kG, bool kNT, int kThreads, bool kOverlap = false>
+template <int kG, bool kNT, int kThreads, bool kOverlap = false, int kAbl = 0>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -817,7 +821,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     const uint64_t gn = g + kPerGroup;
     // the next group is staged inside nfinish, after this group's last row loads; unconditional (past the
     // end it is an empty group of dummy loads: see the wide kernel's step())
-    const uint32_t reg = nfinish<kG, kNT>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
+    const uint32_t reg = nfinish<kG, kNT, kAbl>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
                                           [&]() { take(gn, ib, B); });
     if (j == kNarrowLanes - 1 && g + slot < hi && !ia.over) emit_block(a, g + slot, ~reg);
     load_desc(gn + kPerGroup, dn);  // here, where this group's registers are dead
@@ -1360,6 +1364,8 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
       case 5: crc32c_narrow_kernel<8, true, 768><<<grid, 768, 0, s>>>(a); break;
       case 12: crc32c_narrow_kernel<8, true, 512, true><<<grid, 512, 0, s>>>(a); break;
       case 14: crc32c_narrow_kernel<4, true, 1024, true><<<grid, 1024, 0, s>>>(a); break;
+      case 16: crc32c_narrow_kernel<4, true, 1024, false, 1><<<grid, 1024, 0, s>>>(a); break;  // ablation
+      case 17: crc32c_narrow_kernel<4, true, 512, true, 1><<<grid, 512, 0, s>>>(a); break;    // ablation
 #endif
       case 9: crc32c_narrow_kernel<4, true, 512, true><<<grid, 512, 0, s>>>(a); break;
       default: crc32c_narrow_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
