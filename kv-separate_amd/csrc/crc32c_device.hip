@@ -201,10 +201,12 @@ __device__ __forceinline__ uint4 ld16(uintptr_t addr) {
 template <int kG>
 struct Staged {
   uintptr_t ps, pe, hbase, h0, a1, seg;
-  uint64_t K;     // body rows (0 = no body); the last row ends at a1
+  uint64_t K;     // body rows (0 = no body); the last row ends at ar (kAlign) or a1
   uint4 hc, tc;   // aligned 16 B around the head / the tail
   uint4 v;        // row 0; lanes with v_ok == false (front mask) use zeros instead
   uint4 A[kG];    // rows 1 .. kG (clamped to the last row)
+  uint4 et;       // kAlign: the m full 16-B chunks [ar, a1) in lanes 8-m .. 7
+  uint32_t m;     // kAlign: (a1 - ar) / 16, 0..7
   uintptr_t dummy;  // a valid, cache-resident device address for loads whose data is never used
   bool v_ok;
 };
@@ -212,7 +214,10 @@ struct Staged {
 // Issues a FIXED set of 3 + kG loads whatever the geometry (unneeded ones read `dummy`, a valid
 // device address), so the compiler can wait for exactly this item's loads with a counted vmcnt
 // while the next item's loads stay in flight; masking is deferred to finish().
-template <int kG, bool kNT>
+// kAlign: the rows end at ar = a1 rounded down to 128 B (never below h0), so every row is exactly eight 128-B
+// lines and no line is requested by two rows; the m < 8 whole 16-B chunks between ar and a1 are one extra load
+// (lanes 8-m .. 7) folded by a 3-level lane tree in finish().
+template <int kG, bool kNT, bool kAlign = false>
 __device__ __forceinline__ void stage(Staged<kG>& s, uintptr_t ps, uintptr_t pe, uint32_t lane, uintptr_t dummy,
                                       uint32_t vz) {
   s.ps = ps;
@@ -223,8 +228,16 @@ __device__ __forceinline__ void stage(Staged<kG>& s, uintptr_t ps, uintptr_t pe,
   if (s.h0 > pe) s.h0 = pe;
   s.a1 = pe & ~uintptr_t(15);
   if (s.a1 < s.h0) s.a1 = s.h0;
-  s.K = s.a1 > s.h0 ? (uint64_t(s.a1 - s.h0) + kRowBytes - 1) / kRowBytes : 0;
-  s.seg = s.a1 - s.K * kRowBytes + uintptr_t(lane) * 16u;
+  uintptr_t ar = s.a1;
+  if (kAlign) {
+    ar = s.a1 & ~uintptr_t(127);
+    if (ar < s.h0) ar = s.h0;
+    s.m = uint32_t(s.a1 - ar) >> 4;
+    const bool in = lane < 8 && lane + s.m >= 8;
+    s.et = ld16((in ? s.a1 - 128 + uintptr_t(lane) * 16u : dummy) + vz);
+  }
+  s.K = ar > s.h0 ? (uint64_t(ar - s.h0) + kRowBytes - 1) / kRowBytes : 0;
+  s.seg = ar - s.K * kRowBytes + uintptr_t(lane) * 16u;
   s.v_ok = s.K && s.seg >= s.h0;  // row 0 is front-masked: lanes before h0 hold zeros
   // Head and tail chunks are wave-uniform, but their addresses are offset by the opaque zero `vz` so the
   // compiler keeps them in VGPRs: a provably uniform load result is moved to SGPRs with readfirstlane
@@ -248,7 +261,7 @@ __device__ __forceinline__ void stage(Staged<kG>& s, uintptr_t ps, uintptr_t pe,
 // lets the compiler keep all 16 LDS lookups of a row in flight instead of 2 -- and (b) the next item's
 // loads are the most recent ones, so every wait of this item stays a counted vmcnt that leaves them in
 // flight across the lane merge.
-template <int kG, bool kNT, int kAbl = 0, typename Next>  // kAbl != 0: diagnostic ablations (wrong results)
+template <int kG, bool kNT, int kAbl = 0, bool kAlign = false, typename Next>  // kAbl != 0: ablations (wrong)
 __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, uint32_t reg, uint32_t lane,
                                            uint32_t lc0, uint32_t lc1, Next&& next) {
   if (s.K) {
@@ -336,11 +349,34 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
       const uint32_t m = (2u << j) - 1u;
       if ((lane & m) == m) p = zmap_x(lds, kTreeOff + 4096u * j, o, p);
     }
-    p = uint32_t(__builtin_amdgcn_readlane(int(p), 63));  // pending word at a1 - 4 (wave-uniform)
-    reg = zmap(lds, kZ4Off, p);                              // register at a1
+    p = uint32_t(__builtin_amdgcn_readlane(int(p), 63));  // pending word at the last row's end - 4 (uniform)
+    reg = zmap(lds, kZ4Off, p);                              // register at ar (kAlign) or a1
   } else {
     next();
     if (s.ps < s.h0) reg = serial16(lds, reg, uniform4(s.hc), int(s.ps - s.hbase), int(s.h0 - s.hbase));
+  }
+  if (kAlign && s.m) {
+    // the chunks [ar, a1) right-aligned in lanes 8-m .. 7 (zeros before), the register entering at the first one;
+    // per lane the STEP4W re-injection, then a 3-level tree over lanes 0..7 (Z_16, Z_32, Z_64): lane 7 ends with
+    // the pending word at a1 - 4
+    uint4 e = lane < 8 && lane + s.m >= 8 ? s.et : make_uint4(0, 0, 0, 0);
+    if (lane + s.m == 8) e.x ^= reg;
+    uint32_t p = zmap_x(lds, kZ4Off, e.x, e.y);
+    p = zmap_x(lds, kZ4Off, p, e.z);
+    p = zmap_x(lds, kZ4Off, p, e.w);
+    {
+      const uint32_t o = row_shr<1>(p);
+      if ((lane & 1u) == 1u) p = zmap_x(lds, kTreeOff, o, p);
+    }
+    {
+      const uint32_t o = row_shr<2>(p);
+      if ((lane & 3u) == 3u) p = zmap_x(lds, kTreeOff + 4096u, o, p);
+    }
+    {
+      const uint32_t o = row_shr<4>(p);
+      if ((lane & 7u) == 7u) p = zmap_x(lds, kTreeOff + 8192u, o, p);
+    }
+    reg = zmap(lds, kZ4Off, uint32_t(__builtin_amdgcn_readlane(int(p), 7)));  // register at a1
   }
   if (s.a1 < s.pe) reg = serial16(lds, reg, uniform4(s.tc), 0, int(s.pe - s.a1));
   return reg;
@@ -436,7 +472,8 @@ __device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* rep, cons
 
 // kThreads: 512 (8 waves, 2 per SIMD, <= 256 VGPRs; the default), 768, 1024 or 256 for A/B (launch_pieces_v).
 // One workgroup per CU in every case (the LDS image is 157 KiB).
-template <bool kPlanned, bool kDynamic, int kG, bool kNT, bool kAhead, int kAbl = 0, int kThreads = kWgThreads>
+template <bool kPlanned, bool kDynamic, int kG, bool kNT, bool kAhead, int kAbl = 0, int kThreads = kWgThreads,
+          bool kAlign = true>
 __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -548,7 +585,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
     it.only = rl(w_only) != 0;
     const uintptr_t ps = (uintptr_t(rl(uint32_t(w_ps >> 32))) << 32) | uintptr_t(rl(uint32_t(w_ps)));
     const uintptr_t pe = (uintptr_t(rl(uint32_t(w_pe >> 32))) << 32) | uintptr_t(rl(uint32_t(w_pe)));
-    stage<kG, kNT>(st, ps, pe, lane, reinterpret_cast<uintptr_t>(a.tabs), vz);
+    stage<kG, kNT, kAlign>(st, ps, pe, lane, reinterpret_cast<uintptr_t>(a.tabs), vz);
   };
   auto emit = [&](const Item& it, uint32_t reg) {
     if (lane == 0) {
@@ -573,7 +610,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
     KVSEP_STAMP(t1);
     KVSEP_STAMP(t2);
 #endif
-    emit(ia, finish<kG, kNT, kAbl>(lds, A, ia.reg0, lane, lc0, lc1, [&]() {
+    emit(ia, finish<kG, kNT, kAbl, kAlign>(lds, A, ia.reg0, lane, lc0, lc1, [&]() {
            if (kAhead) take(hn ? g + 1 : g, ib, B);
          }));
 #ifdef KVSEP_STAMPS
@@ -1238,6 +1275,7 @@ void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs
     case 7: crc32c_pieces_kernel<P, D, 8, true, true, 0, 256><<<grid, 256, 0, s>>>(a); break;
     case 8: crc32c_pieces_kernel<P, D, 4, true, true, 1, T><<<grid, T, 0, s>>>(a); break;  // ablation
     case 9: crc32c_pieces_kernel<P, D, 4, true, true, 2, T><<<grid, T, 0, s>>>(a); break;  // ablation
+    case 10: crc32c_pieces_kernel<P, D, 4, true, true, 0, T, false><<<grid, T, 0, s>>>(a); break;  // 16-B rows
 #endif
     default: crc32c_pieces_kernel<P, D, 4, true, true, 0, T><<<grid, T, 0, s>>>(a); break;
   }
