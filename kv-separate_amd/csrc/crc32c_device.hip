@@ -680,7 +680,12 @@ struct NStaged {
   uint4 A[kG];            // rows 1 .. kG (clamped to the last row)
 };
 
-template <int kG, bool kNT>
+// kAlign: a slot's rows end at ar = a1 rounded down to 128 B (never below h0), so every slot row is one whole
+// 128-B line; the m < 8 whole chunks [ar, a1) come in with the tail load: lane j loads a1 - 112 + 16 j, i.e.
+// lanes 7-m .. 6 hold those chunks and lane 7 the partial tail chunk at a1 (the old tc) -- no extra load, no
+// extra registers.  Without it a block at a 16-B but not 128-B aligned address reads two half lines per row
+// (SST blocks in a file image: 20 % slower).
+template <int kG, bool kNT, bool kAlign = true>
 __device__ __forceinline__ void nstage(NStaged<kG>& s, uintptr_t ps, uintptr_t pe, uint32_t j, uintptr_t dummy) {
   s.ps = ps;
   s.pe = pe;
@@ -689,11 +694,21 @@ __device__ __forceinline__ void nstage(NStaged<kG>& s, uintptr_t ps, uintptr_t p
   if (h0 > pe) h0 = pe;
   uintptr_t a1 = pe & ~uintptr_t(15);
   if (a1 < h0) a1 = h0;
-  s.K = a1 > h0 ? uint32_t((a1 - h0 + kNarrowRow - 1) / kNarrowRow) : 0u;
-  s.seg = a1 - uintptr_t(s.K) * kNarrowRow + uintptr_t(j) * 16u;
+  uintptr_t ar = a1;
+  if (kAlign) {
+    ar = a1 & ~uintptr_t(127);
+    if (ar < h0) ar = h0;
+  }
+  s.K = ar > h0 ? uint32_t((ar - h0 + kNarrowRow - 1) / kNarrowRow) : 0u;
+  s.seg = ar - uintptr_t(s.K) * kNarrowRow + uintptr_t(j) * 16u;
   const bool v_ok = s.K && s.seg >= h0;
   s.hc = ld16(ps < h0 ? hbase : dummy);
-  s.tc = ld16(a1 < pe ? a1 : dummy);
+  if (kAlign) {
+    const uint32_t m = uint32_t(a1 - ar) >> 4;
+    s.tc = ld16((j == kNarrowLanes - 1 ? a1 < pe : j + m >= kNarrowLanes - 1) ? a1 - 112 + uintptr_t(j) * 16u : dummy);
+  } else {
+    s.tc = ld16(a1 < pe ? a1 : dummy);
+  }
   s.v = ld16<kNT>(v_ok ? s.seg : dummy);
   const uint32_t last = s.K > 1 ? s.K - 1 : 0;
 #pragma unroll
@@ -703,7 +718,7 @@ __device__ __forceinline__ void nstage(NStaged<kG>& s, uintptr_t ps, uintptr_t p
 
 // Raw register after the slot item, valid in the slot's last lane (j == 7).  kmin / kmax: wave min / max of K.
 // `next()` stages the following group, after this group's last row loads (see the wide kernel's finish()).
-template <int kG, bool kNT, int kAbl = 0, typename Next>  // kAbl != 0: KVSEP_DIAG ablation (wrong results)
+template <int kG, bool kNT, int kAbl = 0, bool kAlign = true, typename Next>  // kAbl != 0: ablation (wrong)
 __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, uint32_t reg, uint32_t j,
                                             uint32_t lc0, uint32_t lc1, uint32_t kmin, uint32_t kmax,
                                             uintptr_t dummy, Next&& next) {
@@ -712,6 +727,11 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
   if (h0 > s.pe) h0 = s.pe;
   uintptr_t a1 = s.pe & ~uintptr_t(15);
   if (a1 < h0) a1 = h0;
+  uintptr_t ar = a1;
+  if (kAlign) {
+    ar = a1 & ~uintptr_t(127);
+    if (ar < h0) ar = h0;
+  }
   if (!kmax) next();
   if (s.ps < h0) reg = serial16(lds, reg, s.hc, int(s.ps - hbase), int(h0 - hbase));
   if (kmax) {
@@ -775,14 +795,44 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
       const uint32_t o = row_shr<4>(p);
       if ((j & 7u) == 7u) p = zmap_x(lds, kTreeOff + 8192u, o, p);
     }
-    if (K) reg = zmap(lds, kZ4Off, p);  // lane 7 of the slot: pending word at a1 - 4 -> register at a1
+    if (K) reg = zmap(lds, kZ4Off, p);  // lane 7 of the slot: pending word at the rows' end - 4 -> register there
   }
-  if (a1 < s.pe) reg = serial16(lds, reg, s.tc, 0, int(s.pe - a1));
+  if (kAlign) {
+    const uint32_t m = uint32_t(a1 - ar) >> 4;  // whole chunks [ar, a1) in lanes 7-m .. 6 of the tail load
+    if (__builtin_amdgcn_ballot_w64(m != 0)) {
+      // their raw register from 0: per lane the STEP4W re-injection, moved up one lane (chunks in lanes 8-m .. 7),
+      // the slot's 3-level tree; then R = Z_16m(register at ar) ^ that (Z_16m from the tree tables by the bits of m)
+      const uint4 e = j < kNarrowLanes - 1 && j + m >= kNarrowLanes - 1 ? s.tc : make_uint4(0, 0, 0, 0);
+      uint32_t p = zmap_x(lds, kZ4Off, e.x, e.y);
+      p = zmap_x(lds, kZ4Off, p, e.z);
+      p = zmap_x(lds, kZ4Off, p, e.w);
+      p = j == 0 ? 0u : row_shr<1>(p);
+      {
+        const uint32_t o = row_shr<1>(p);
+        if ((j & 1u) == 1u) p = zmap_x(lds, kTreeOff, o, p);
+      }
+      {
+        const uint32_t o = row_shr<2>(p);
+        if ((j & 3u) == 3u) p = zmap_x(lds, kTreeOff + 4096u, o, p);
+      }
+      {
+        const uint32_t o = row_shr<4>(p);
+        if ((j & 7u) == 7u) p = zmap_x(lds, kTreeOff + 8192u, o, p);
+      }
+      if (m & 1u) reg = zmap(lds, kTreeOff, reg);
+      if (m & 2u) reg = zmap(lds, kTreeOff + 4096u, reg);
+      if (m & 4u) reg = zmap(lds, kTreeOff + 8192u, reg);
+      reg ^= zmap(lds, kZ4Off, p);  // lane 7: register at a1
+    }
+    if (a1 < s.pe) reg = serial16(lds, reg, s.tc, 0, int(s.pe - a1));  // lane 7's tail load is the chunk at a1
+  } else {
+    if (a1 < s.pe) reg = serial16(lds, reg, s.tc, 0, int(s.pe - a1));
+  }
   return reg;
 }
 
 // Unsplit batches only (every block <= 64 KiB <= piece_bytes); static contiguous runs of 8-block groups.
-template <int kG, bool kNT, int kThreads, bool kOverlap = false, int kAbl = 0>
+template <int kG, bool kNT, int kThreads, bool kOverlap = false, int kAbl = 0, bool kAlignN = true>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -843,7 +893,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     const uintptr_t ps = live ? reinterpret_cast<uintptr_t>(a.base) + dn.off : dummy;
     it.reg0 = ~dn.init;
     it.over = over;
-    nstage<kG, kNT>(st, ps, ps + (live ? dn.len : 0u), j, dummy);
+    nstage<kG, kNT, kAlignN>(st, ps, ps + (live ? dn.len : 0u), j, dummy);
     uint32_t km = 0, kn = ~0u;
 #pragma unroll
     for (uint32_t k = 0; k < kPerGroup; ++k) {
@@ -858,7 +908,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     const uint64_t gn = g + kPerGroup;
     // the next group is staged inside nfinish, after this group's last row loads; unconditional (past the
     // end it is an empty group of dummy loads: see the wide kernel's step())
-    const uint32_t reg = nfinish<kG, kNT, kAbl>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
+    const uint32_t reg = nfinish<kG, kNT, kAbl, kAlignN>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
                                           [&]() { take(gn, ib, B); });
     if (j == kNarrowLanes - 1 && g + slot < hi && !ia.over) emit_block(a, g + slot, ~reg);
     load_desc(gn + kPerGroup, dn);  // here, where this group's registers are dead
@@ -943,7 +993,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
         const uint64_t rs = uint64_t(slot) * q, re = slot == kPerGroup - 1 ? L : rs + q;
         const uintptr_t blk = reinterpret_cast<uintptr_t>(a.base) + boff;
         NStaged<kG> X;
-        nstage<kG, kNT>(X, blk + rs, blk + re, j, dummy);
+        nstage<kG, kNT, kAlignN>(X, blk + rs, blk + re, j, dummy);
         uint32_t km = 0, kn = ~0u;
 #pragma unroll
         for (uint32_t t = 0; t < kPerGroup; ++t) {
@@ -951,7 +1001,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
           km = km > kk ? km : kk;
           kn = kn < kk ? kn : kk;
         }
-        uint32_t reg = nfinish<kG, kNT>(lds, X, slot == 0 ? ~binit : 0u, j, lc0, lc1, kn, km, dummy, NoMid());
+        uint32_t reg = nfinish<kG, kNT, 0, kAlignN>(lds, X, slot == 0 ? ~binit : 0u, j, lc0, lc1, kn, km, dummy,
+                                                    NoMid());
         if (j == kNarrowLanes - 1) reg = gf2_shift(a.tabs, reg, L - re);  // carried to the block's end
         uint32_t acc = 0;
 #pragma unroll
@@ -1403,6 +1454,8 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
       case 12: crc32c_narrow_kernel<8, true, 512, true><<<grid, 512, 0, s>>>(a); break;
       case 14: crc32c_narrow_kernel<4, true, 1024, true><<<grid, 1024, 0, s>>>(a); break;
       case 16: crc32c_narrow_kernel<4, true, 1024, false, 1><<<grid, 1024, 0, s>>>(a); break;  // ablation
+      case 18: crc32c_narrow_kernel<4, true, 1024, false, 0, false><<<grid, 1024, 0, s>>>(a); break;  // 16-B rows
+      case 19: crc32c_narrow_kernel<4, true, 512, true, 0, false><<<grid, 512, 0, s>>>(a); break;     // 16-B rows
       case 17: crc32c_narrow_kernel<4, true, 512, true, 1><<<grid, 512, 0, s>>>(a); break;    // ablation
 #endif
       case 9: crc32c_narrow_kernel<4, true, 512, true><<<grid, 512, 0, s>>>(a); break;
