@@ -727,10 +727,15 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
   if (h0 > s.pe) h0 = s.pe;
   uintptr_t a1 = s.pe & ~uintptr_t(15);
   if (a1 < h0) a1 = h0;
-  uintptr_t ar = a1;
+  // what the end needs, as two 32-bit values computed here: live across the row loop in place of 64-bit a1 / ar
+  // (at 16 waves the kernel sits at 128 VGPRs, and a spilled lane constant reloaded per group waits vmcnt(0) --
+  // draining the next group's row loads)
+  // bits 0-3: bytes after a1; bits 4-6 (kAlign): m, the whole chunks [ar, a1), ar = max(a1 & ~127, h0)
+  uint32_t endg = uint32_t(s.pe - a1);
   if (kAlign) {
-    ar = a1 & ~uintptr_t(127);
-    if (ar < h0) ar = h0;
+    const uint64_t d = a1 - h0;
+    const uint32_t r = uint32_t(a1) & 127u;
+    endg |= (d < r ? uint32_t(d) : r) & 0x70u;
   }
   if (!kmax) next();
   if (s.ps < h0) reg = serial16(lds, reg, s.hc, int(s.ps - hbase), int(h0 - hbase));
@@ -798,15 +803,15 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
     if (K) reg = zmap(lds, kZ4Off, p);  // lane 7 of the slot: pending word at the rows' end - 4 -> register there
   }
   if (kAlign) {
-    const uint32_t m = uint32_t(a1 - ar) >> 4;  // whole chunks [ar, a1) in lanes 7-m .. 6 of the tail load
-    if (__builtin_amdgcn_ballot_w64(m != 0)) {
+    const uint32_t m = endg >> 4;
+    if (__builtin_amdgcn_ballot_w64(m != 0)) {  // whole chunks [ar, a1) in lanes 7-m .. 6 of the tail load
       // their raw register from 0: per lane the STEP4W re-injection, moved up one lane (chunks in lanes 8-m .. 7),
       // the slot's 3-level tree; then R = Z_16m(register at ar) ^ that (Z_16m from the tree tables by the bits of m)
       const uint4 e = j < kNarrowLanes - 1 && j + m >= kNarrowLanes - 1 ? s.tc : make_uint4(0, 0, 0, 0);
       uint32_t p = zmap_x(lds, kZ4Off, e.x, e.y);
       p = zmap_x(lds, kZ4Off, p, e.z);
       p = zmap_x(lds, kZ4Off, p, e.w);
-      p = j == 0 ? 0u : row_shr<1>(p);
+      p = row_shr<1>(p);  // lane 8k + 7 holds no chunk (its e is zero, so p is zero): slot k+1's lane 0 gets 0
       {
         const uint32_t o = row_shr<1>(p);
         if ((j & 1u) == 1u) p = zmap_x(lds, kTreeOff, o, p);
@@ -824,10 +829,8 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
       if (m & 4u) reg = zmap(lds, kTreeOff + 8192u, reg);
       reg ^= zmap(lds, kZ4Off, p);  // lane 7: register at a1
     }
-    if (a1 < s.pe) reg = serial16(lds, reg, s.tc, 0, int(s.pe - a1));  // lane 7's tail load is the chunk at a1
-  } else {
-    if (a1 < s.pe) reg = serial16(lds, reg, s.tc, 0, int(s.pe - a1));
   }
+  if (endg & 15u) reg = serial16(lds, reg, s.tc, 0, int(endg & 15u));  // lane 7's tail load is the chunk at a1
   return reg;
 }
 
@@ -869,7 +872,11 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     uint32_t len, lenhi, init;
   };
   auto load_desc = [&](uint64_t g, Desc& d) {  // block g + slot; past hi: loads stay in bounds, take() empties it
-    const uint64_t b = g + slot;
+    // slot through an empty asm: otherwise (g + 16 + slot) becomes a hoisted 64-bit lane constant that, at 128
+    // VGPRs, is spilled and reloaded per group with a vmcnt(0) wait that drains the next group's row loads
+    uint32_t sl = slot;
+    asm volatile("" : "+v"(sl));
+    const uint64_t b = g + sl;
     const uint64_t bb = b < hi ? b : hi - 1;
     d.off = a.off[bb];
     const uint2 l = *reinterpret_cast<const uint2*>(a.len + bb);  // one 8-B load, both words consumed at the take

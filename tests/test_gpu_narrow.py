@@ -112,3 +112,29 @@ def test_verify_mode_narrow(ctxs, oracle, pool):
     torch.cuda.synchronize()
     assert fb.item() == 17 and nb.item() == 3
     assert np.array_equal(out.cpu().numpy().view(np.uint32), crc)
+
+
+@pytest.mark.parametrize("kernel", ["narrow16", "narrow8"])
+def test_every_end_geometry(oracle, pool, kernel):
+    """Every case of the slot's end path: m = 0..7 whole 16-B chunks between the 128-B grid and the 16-B end (m = 7
+    uses all of lanes 0..6 of the tail load), each with head and tail bytes 0..15, with and without body rows."""
+    data, d = pool
+    ctx = kvsep.Context(0)
+    ctx.set_kernel(kernel)
+    ps, pe = [], []
+    for rows in (-1, 0, 1, 3):  # -1: no row on the grid (a1 = h0 + 16 m)
+        for m in range(8):
+            for head in range(16):
+                for tail in (0, 1, 7, 15):
+                    start = 1024 * len(ps) + 16 + 128 - head  # ps % 16 == (16 - head) % 16: `head` head bytes
+                    h0 = start + head
+                    a1 = h0 + 16 * m if rows < 0 else ((h0 + 127) // 128 + rows) * 128 + 16 * m
+                    ps.append(start)
+                    pe.append(a1 + tail)
+    off = np.array(ps, np.uint64)
+    ln = np.array(pe, np.uint64) - off
+    assert int(off[-1] + ln[-1]) < data.size
+    init = np.arange(off.size, dtype=np.uint32) * np.uint32(2654435761)
+    got = run(ctx, d, off, ln, init=init)
+    ctx.close()
+    assert np.array_equal(got, oracle.batch(data, off, ln, init))
