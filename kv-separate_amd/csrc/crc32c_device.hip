@@ -674,8 +674,9 @@ constexpr uint64_t kNarrowMax = 32 * 1024;  // longest block the narrow kernel i
 
 template <int kG>
 struct NStaged {
-  uintptr_t ps, pe, seg;  // this lane's slot item [ps, pe); its 16-B chunk of row 0
-  uint32_t K;             // body rows of the slot item
+  uintptr_t ps, seg;  // this lane's slot item [ps, ps + len); its 16-B chunk of row 0
+  uint32_t len;       // < 2^31: <= the hint (<= 64 KiB) on the main path, <= 1 GiB parts on the deferred one
+  uint32_t K;         // body rows of the slot item
   uint4 hc, tc, v;
   uint4 A[kG];            // rows 1 .. kG (clamped to the last row)
 };
@@ -685,29 +686,46 @@ struct NStaged {
 // lanes 7-m .. 6 hold those chunks and lane 7 the partial tail chunk at a1 (the old tc) -- no extra load, no
 // extra registers.  Without it a block at a 16-B but not 128-B aligned address reads two half lines per row
 // (SST blocks in a file image: 20 % slower).
-template <int kG, bool kNT, bool kAlign = true>
-__device__ __forceinline__ void nstage(NStaged<kG>& s, uintptr_t ps, uintptr_t pe, uint32_t j, uintptr_t dummy) {
-  s.ps = ps;
-  s.pe = pe;
-  const uintptr_t hbase = ps & ~uintptr_t(15);
-  uintptr_t h0 = (ps + 15) & ~uintptr_t(15);
-  if (h0 > pe) h0 = pe;
-  uintptr_t a1 = pe & ~uintptr_t(15);
-  if (a1 < h0) a1 = h0;
-  uintptr_t ar = a1;
+// The slot geometry in 32-bit offsets from the 128-B line holding ps (len < 2^31, so nothing wraps): P = ps's
+// offset in that line, E = the end, h0 / a1 = the first / last 16-B boundary inside [P, E] (clamped), ar = where
+// the rows end.  64-bit address arithmetic only for the loads.
+struct NGeo {
+  uint32_t P, E, h0, a1, ar;
+};
+template <bool kAlign>
+__device__ __forceinline__ NGeo ngeo(uintptr_t ps, uint32_t len) {
+  NGeo g;
+  g.P = uint32_t(ps) & (kNarrowRow - 1);
+  g.E = g.P + len;
+  g.h0 = (g.P + 15u) & ~15u;
+  if (g.h0 > g.E) g.h0 = g.E;
+  g.a1 = g.E & ~15u;
+  if (g.a1 < g.h0) g.a1 = g.h0;
+  g.ar = g.a1;
   if (kAlign) {
-    ar = a1 & ~uintptr_t(127);
-    if (ar < h0) ar = h0;
+    g.ar = g.a1 & ~(kNarrowRow - 1);
+    if (g.ar < g.h0) g.ar = g.h0;
   }
-  s.K = ar > h0 ? uint32_t((ar - h0 + kNarrowRow - 1) / kNarrowRow) : 0u;
-  s.seg = ar - uintptr_t(s.K) * kNarrowRow + uintptr_t(j) * 16u;
-  const bool v_ok = s.K && s.seg >= h0;
-  s.hc = ld16(ps < h0 ? hbase : dummy);
+  return g;
+}
+
+template <int kG, bool kNT, bool kAlign = true>
+__device__ __forceinline__ void nstage(NStaged<kG>& s, uintptr_t ps, uint32_t len, uint32_t j, uintptr_t dummy) {
+  s.ps = ps;
+  s.len = len;
+  const NGeo g = ngeo<kAlign>(ps, len);
+  const uintptr_t line = ps - g.P;
+  s.K = (g.ar - g.h0 + kNarrowRow - 1) / kNarrowRow;
+  const int32_t rel0 = int32_t(g.ar - s.K * kNarrowRow + j * 16u);  // row 0's chunk, may start before the line
+  s.seg = line + intptr_t(rel0);
+  const bool v_ok = s.K && rel0 >= int32_t(g.h0);
+  s.hc = ld16(g.P < g.h0 ? line + (g.P & ~15u) : dummy);
   if (kAlign) {
-    const uint32_t m = uint32_t(a1 - ar) >> 4;
-    s.tc = ld16((j == kNarrowLanes - 1 ? a1 < pe : j + m >= kNarrowLanes - 1) ? a1 - 112 + uintptr_t(j) * 16u : dummy);
+    const uint32_t m = (g.a1 - g.ar) >> 4;
+    s.tc = ld16((j == kNarrowLanes - 1 ? g.a1 < g.E : j + m >= kNarrowLanes - 1) ? line + (g.a1 - 112u + j * 16u)
+                                                                                 : dummy);
   } else {
-    s.tc = ld16(a1 < pe ? a1 : dummy);
+    s.tc = ld16(g.a1 < g.E ? line + g.a1 : dummy);
   }
   s.v = ld16<kNT>(v_ok ? s.seg : dummy);
   const uint32_t last = s.K > 1 ? s.K - 1 : 0;
@@ -722,27 +740,17 @@ template <int kG, bool kNT, int kAbl = 0, bool kAlign = true, typename Next>  //
 __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, uint32_t reg, uint32_t j,
                                             uint32_t lc0, uint32_t lc1, uint32_t kmin, uint32_t kmax,
                                             uintptr_t dummy, Next&& next) {
-  const uintptr_t hbase = s.ps & ~uintptr_t(15);
-  uintptr_t h0 = (s.ps + 15) & ~uintptr_t(15);
-  if (h0 > s.pe) h0 = s.pe;
-  uintptr_t a1 = s.pe & ~uintptr_t(15);
-  if (a1 < h0) a1 = h0;
-  // what the end needs, as two 32-bit values computed here: live across the row loop in place of 64-bit a1 / ar
-  // (at 16 waves the kernel sits at 128 VGPRs, and a spilled lane constant reloaded per group waits vmcnt(0) --
-  // draining the next group's row loads)
-  // bits 0-3: bytes after a1; bits 4-6 (kAlign): m, the whole chunks [ar, a1), ar = max(a1 & ~127, h0)
-  uint32_t endg = uint32_t(s.pe - a1);
-  if (kAlign) {
-    const uint64_t d = a1 - h0;
-    const uint32_t r = uint32_t(a1) & 127u;
-    endg |= (d < r ? uint32_t(d) : r) & 0x70u;
-  }
+  const NGeo g = ngeo<kAlign>(s.ps, s.len);
+  // what the end needs, packed in one 32-bit value computed here, live across the row loop (at 16 waves the kernel
+  // sits at 128 VGPRs): bits 0-3 the bytes after a1, bits 4-6 (kAlign) m, the whole chunks [ar, a1)
+  const uint32_t endg = (g.E - g.a1) | (g.a1 - g.ar);
+  const int32_t rel0 = int32_t(uint32_t(s.seg) - uint32_t(s.ps) + g.P);  // row 0's chunk from the line (as staged)
   if (!kmax) next();
-  if (s.ps < h0) reg = serial16(lds, reg, s.hc, int(s.ps - hbase), int(h0 - hbase));
+  if (g.P < g.h0) reg = serial16(lds, reg, s.hc, int(g.P & 15u), int(g.h0 - (g.P & ~15u)));
   if (kmax) {
     const uint32_t K = s.K, last = K > 1 ? K - 1 : 0;
-    uint4 v = (K && s.seg >= h0) ? s.v : make_uint4(0, 0, 0, 0);
-    if (K && s.seg == h0) v.x ^= reg;  // the head register enters as pending word at h0
+    uint4 v = (K && rel0 >= int32_t(g.h0)) ? s.v : make_uint4(0, 0, 0, 0);
+    if (K && rel0 == int32_t(g.h0)) v.x ^= reg;  // the head register enters as pending word at h0
     uint32_t c0 = v.x, c1 = v.y, c2 = v.z, c3 = v.w;
 #define KVSEP_NROW(V)                                                 \
   do {                                                                \
@@ -900,7 +908,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     const uintptr_t ps = live ? reinterpret_cast<uintptr_t>(a.base) + dn.off : dummy;
     it.reg0 = ~dn.init;
     it.over = over;
-    nstage<kG, kNT, kAlignN>(st, ps, ps + (live ? dn.len : 0u), j, dummy);
+    nstage<kG, kNT, kAlignN>(st, ps, live ? dn.len : 0u, j, dummy);
     uint32_t km = 0, kn = ~0u;
 #pragma unroll
     for (uint32_t k = 0; k < kPerGroup; ++k) {
@@ -996,25 +1004,33 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
         const uint64_t L = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(d.lenhi), int(src)))) << 32) |
                            uint32_t(__builtin_amdgcn_readlane(int(d.len), int(src)));
         const uint32_t binit = uint32_t(__builtin_amdgcn_readlane(int(d.init), int(src)));
-        const uint64_t q = L / kPerGroup;
-        const uint64_t rs = uint64_t(slot) * q, re = slot == kPerGroup - 1 ? L : rs + q;
+        // parts of q <= 1 GiB bytes (the slot geometry is 32-bit), 8 at a time, one per slot; part p's raw register
+        // (from ~init for part 0, from 0 for the others) is carried to the block's end and the parts XORed
+        uint64_t q = (L + kPerGroup - 1) / kPerGroup;
+        if (q > (1ull << 30)) q = 1ull << 30;
+        const uint64_t nparts = (L + q - 1) / q;
         const uintptr_t blk = reinterpret_cast<uintptr_t>(a.base) + boff;
-        NStaged<kG> X;
-        nstage<kG, kNT, kAlignN>(X, blk + rs, blk + re, j, dummy);
-        uint32_t km = 0, kn = ~0u;
-#pragma unroll
-        for (uint32_t t = 0; t < kPerGroup; ++t) {
-          const uint32_t kk = uint32_t(__builtin_amdgcn_readlane(int(X.K), int(t * kNarrowLanes)));
-          km = km > kk ? km : kk;
-          kn = kn < kk ? kn : kk;
-        }
-        uint32_t reg = nfinish<kG, kNT, 0, kAlignN>(lds, X, slot == 0 ? ~binit : 0u, j, lc0, lc1, kn, km, dummy,
-                                                    NoMid());
-        if (j == kNarrowLanes - 1) reg = gf2_shift(a.tabs, reg, L - re);  // carried to the block's end
         uint32_t acc = 0;
+        for (uint64_t p0 = 0; p0 < nparts; p0 += kPerGroup) {
+          const uint64_t p = p0 + slot;
+          const uint64_t rs = p < nparts ? p * q : L;
+          const uint64_t re = rs + q < L ? rs + q : L;
+          NStaged<kG> X;
+          nstage<kG, kNT, kAlignN>(X, blk + rs, uint32_t(re - rs), j, dummy);
+          uint32_t km = 0, kn = ~0u;
 #pragma unroll
-        for (uint32_t t = 0; t < kPerGroup; ++t)
-          acc ^= uint32_t(__builtin_amdgcn_readlane(int(reg), int(t * kNarrowLanes + kNarrowLanes - 1)));
+          for (uint32_t t = 0; t < kPerGroup; ++t) {
+            const uint32_t kk = uint32_t(__builtin_amdgcn_readlane(int(X.K), int(t * kNarrowLanes)));
+            km = km > kk ? km : kk;
+            kn = kn < kk ? kn : kk;
+          }
+          uint32_t reg = nfinish<kG, kNT, 0, kAlignN>(lds, X, p == 0 ? ~binit : 0u, j, lc0, lc1, kn, km, dummy,
+                                                      NoMid());
+          if (j == kNarrowLanes - 1) reg = gf2_shift(a.tabs, reg, L - re);  // carried to the block's end
+#pragma unroll
+          for (uint32_t t = 0; t < kPerGroup; ++t)
+            acc ^= uint32_t(__builtin_amdgcn_readlane(int(reg), int(t * kNarrowLanes + kNarrowLanes - 1)));
+        }
         if (lane == 0) emit_block(a, g + k, ~acc);
       }
     }

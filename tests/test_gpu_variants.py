@@ -93,10 +93,11 @@ def test_understated_hint_is_exact(ragged, kernel):
         ctx.close()
 
 
-def test_understated_hint_block_over_4gib(oracle):
+@pytest.mark.parametrize("n", [(1 << 32) + 77, (9 << 30) + 5])
+def test_understated_hint_block_over_4gib(oracle, n):
     """A 2^32 + 77-byte block among 4 KiB blocks under a 4 KiB hint, on the narrow kernel: its length does not fit
-    the narrow kernel's 32-bit staging, so it must take the deferred path with its full 64-bit length."""
-    n = (1 << 32) + 77
+    the narrow kernel's 32-bit staging, so it must take the deferred path with its full 64-bit length.  At 9 GiB + 5
+    the deferred path cuts it into 10 parts of <= 1 GiB, two rounds of 8 slots."""
     buf = torch.empty(n + 4096 * 64 + 64, dtype=torch.uint8, device=DEV)
     kvsep.fill_splitmix64(buf.data_ptr(), buf.numel(), 4242, 0)
     ctx = kvsep.Context(0)
