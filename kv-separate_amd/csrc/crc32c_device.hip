@@ -266,7 +266,7 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
                                            uint32_t lc0, uint32_t lc1, Next&& next) {
   if (s.K) {
     const uint64_t K = s.K, last = K - 1;
-    if (s.ps < s.h0) reg = serial16(lds, reg, uniform4(s.hc), int(s.ps - s.hbase), int(s.h0 - s.hbase));
+    if (kAbl != 3 && s.ps < s.h0) reg = serial16(lds, reg, uniform4(s.hc), int(s.ps - s.hbase), int(s.h0 - s.hbase));
     uint4 v = s.v_ok ? s.v : make_uint4(0, 0, 0, 0);
     if (s.seg == s.h0) v.x ^= reg;  // the head register enters as pending word at h0
     uint32_t c0 = v.x, c1 = v.y, c2 = v.z, c3 = v.w;
@@ -329,7 +329,7 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     // The partner of an active lane l is l - 2^j: DPP row_shr for j < 4 (within a 16-lane row), lane
     // reads for j = 4, 5 -- no ds_bpermute round trips on this latency-bound chain.
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
+    for (int j = 0; j < (kAbl == 4 ? 0 : 6); ++j) {
       uint32_t o;
       if (j == 0) {
         o = row_shr<1>(p);
@@ -353,7 +353,7 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     reg = zmap(lds, kZ4Off, p);                              // register at ar (kAlign) or a1
   } else {
     next();
-    if (s.ps < s.h0) reg = serial16(lds, reg, uniform4(s.hc), int(s.ps - s.hbase), int(s.h0 - s.hbase));
+    if (kAbl != 3 && s.ps < s.h0) reg = serial16(lds, reg, uniform4(s.hc), int(s.ps - s.hbase), int(s.h0 - s.hbase));
   }
   if (kAlign && s.m) {
     // the chunks [ar, a1) right-aligned in lanes 8-m .. 7 (zeros before), the register entering at the first one;
@@ -378,7 +378,7 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     }
     reg = zmap(lds, kZ4Off, uint32_t(__builtin_amdgcn_readlane(int(p), 7)));  // register at a1
   }
-  if (s.a1 < s.pe) reg = serial16(lds, reg, uniform4(s.tc), 0, int(s.pe - s.a1));
+  if (kAbl != 3 && s.a1 < s.pe) reg = serial16(lds, reg, uniform4(s.tc), 0, int(s.pe - s.a1));
   return reg;
 }
 
@@ -1350,6 +1350,8 @@ void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs
     case 8: crc32c_pieces_kernel<P, D, 4, true, true, 1, T><<<grid, T, 0, s>>>(a); break;  // ablation
     case 9: crc32c_pieces_kernel<P, D, 4, true, true, 2, T><<<grid, T, 0, s>>>(a); break;  // ablation
     case 10: crc32c_pieces_kernel<P, D, 4, true, true, 0, T, false><<<grid, T, 0, s>>>(a); break;  // 16-B rows
+    case 11: crc32c_pieces_kernel<P, D, 4, true, true, 3, T><<<grid, T, 0, s>>>(a); break;  // ablation: no head/tail
+    case 12: crc32c_pieces_kernel<P, D, 4, true, true, 4, T><<<grid, T, 0, s>>>(a); break;  // ablation: no lane tree
 #endif
     default: crc32c_pieces_kernel<P, D, 4, true, true, 0, T><<<grid, T, 0, s>>>(a); break;
   }

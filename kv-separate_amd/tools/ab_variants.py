@@ -5,7 +5,8 @@ usage: python ab_variants.py --variants 1,2 --configs 3a,2 --rounds 5 --steps 5
 Prints per (config, variant) the median / min kernel time and GB/s (kernel-only HIP events).
 A variant written "b<N>" runs variant N of a second build of the library (--lib-b), so two source versions
 are compared in one process on one box; "n<K>" selects narrow-kernel variant K (KVSEP_NARROW) for short blocks;
-"<N>p<KiB>" runs variant N with its own piece size; a trailing "s" / "d" forces the static / guided schedule.
+"<N>p<KiB>" runs variant N with its own piece size; a trailing "s" / "d" forces the static / guided schedule, and a
+final "w" the wide kernel.
 """
 import argparse
 import os
@@ -29,6 +30,9 @@ def layout(cfg):
         m = re.fullmatch(r"u(\d+)x(\d+)(?:s(\d+))?(?:f(\d+))?", cfg)
         count, length, stride, first = m.groups()
         return W.uniform_layout(int(count), int(length), int(stride) if stride else None, int(first or 0))
+    if cfg == "4s":  # config 4's blocks of <= 32 KiB only (86 % of its blocks, 1 % of its bytes)
+        off, ln = W.cfg4_layout()
+        return off[ln <= 32768], ln[ln <= 32768]
     return {"3a": W.cfg3_layout, "3b": lambda: W.cfg3_layout(vlog=True), "2": W.cfg2_layout,
             "4": W.cfg4_layout}[cfg]()
 
@@ -59,6 +63,9 @@ def main():
         code = v[1:] if v.startswith("b") else v
         piece_kib = args.piece_kib
         sched = None
+        wide = code.endswith("w")  # "<variant>w": the wide kernel even where the narrow one would be chosen
+        if wide:
+            code = code[:-1]
         if code.endswith("s") or code.endswith("d"):  # "<variant>s" / "<variant>d": static / guided schedule
             sched, code = code[-1] == "d", code[:-1]
         if "p" in code:  # "<variant>p<KiB>": that variant with its own piece size, e.g. 1p128 vs 1p1024
@@ -73,6 +80,8 @@ def main():
             ctxs[v].set_piece_bytes(piece_kib * 1024)
         if sched is not None:
             ctxs[v].set_schedule(sched)
+        if wide:
+            ctxs[v].set_kernel("wide")
     dev = torch.device("cuda:0")
     for cfg in args.configs.split(","):
         off, ln = layout(cfg)
