@@ -661,7 +661,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
 
 // ------------------------------------------------------------------------------------------------
 // Narrow kernel for batches of many short blocks (use_narrow): a wavefront runs 8 blocks at once,
-// kNarrowLanes = 8 lanes ("a slot") per block and rows of 128 B ending at the block's aligned end.  The wide
+// kNarrowLanes = 8 lanes ("a slot") per block and rows of 128 B on the 128-B address grid (see nstage).  The wide
 // kernel pays a fixed cost per block (lane merge, 6-level lane tree, staging: ~230 of its ~313 VALU
 // instructions for a 4 KiB block, PMC SQ_INSTS_VALU); here the merge is a 3-level tree inside the slot and
 // staging is shared by the 8 blocks, so the cost per block is mostly the fold itself.  The chain fold uses
@@ -1332,12 +1332,13 @@ void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs
   // item staged ahead.  On one MI355X, interleaved in one process (tools/ab_variants.py), 8 waves beat 16 waves
   // by 1.5-2 % on 1 MiB blocks and by 4-5 % on the Zipf batch; 12 waves sit between.  The others are for A/B:
   //   0: plain loads    2: no staging ahead    3: 8-row groups
-  // (a 3-slot ring of row groups, 8 rows in flight, and a 128-B aligned row grid that re-reads no line were
-  // both tried and measured slower: -2 to -7 % and -2 to -4 %; the extra VGPRs cost LDS-lookup overlap)
+  // (a 3-slot ring of row groups, 8 rows in flight, was tried and measured -2 to -7 %: the extra VGPRs cost
+  // LDS-lookup overlap; so was staging items two ahead, -1.5 % on the Zipf batch)
   //   5: 16-wave workgroups (the round-1 kernel)    6: 12-wave workgroups    7: 4-wave workgroups, 8-row groups
-  //   8, 9: diagnostic ablations (wrong results)
+  //   10: rows ending at the 16-B aligned end (before the 128-B grid)
+  //   8, 9, 11, 12: diagnostic ablations (wrong results): no lane merge, XOR folds, no head/tail steps, no tree
   // Only the default is compiled into the shipped library; the rest exist in the KVSEP_DIAG tools build
-  // (`make -C kv-separate_amd diag` -> tools/libkvsep_diag.so), and 8 and 9 give wrong results by design.
+  // (`make -C kv-separate_amd diag` -> tools/libkvsep_diag.so).
   constexpr int T = kWgThreads;
   switch (variant) {
 #ifdef KVSEP_DIAG

@@ -1,7 +1,7 @@
 """Point the kvsep binding at the KVSEP_DIAG tools build (tools/libkvsep_diag.so, `make -C kv-separate_amd diag`).
 
 That build carries the A/B and ablation kernel variants (selected by KVSEP_CRC_VARIANT / KVSEP_NARROW /
-KVSEP_CRC_STATIC_RR; variants 8 and 9 give wrong results by design).  The shipped library has none of them and
+KVSEP_CRC_STATIC_RR; the ablation variants give wrong results by design).  The shipped library has none of them and
 reads none of those variables.  Import this module before the first kvsep call of a diagnostic tool."""
 import os
 import subprocess
