@@ -81,6 +81,9 @@ struct PiecesArgs {
   const uint32_t* zpiece;           // Z_piece_bytes as 4 byte tables (combine kernel)
   uint64_t max_pieces;              // capacity of pblk/partial
   uint32_t static_contig;           // static schedule: contiguous item ranges per wave (else round-robin)
+  uint32_t guided_div;              // dynamic schedule: a grab takes remaining / (guided_div * nwaves) items;
+                                    // 0: adaptive, clamp(total / (64 * nwaves), 4, 32)
+  uint32_t guided_cap;              // dynamic schedule: at most this many items per grab (0: no cap)
   uint64_t hint;                    // narrow kernel: the caller's max_len hint; longer blocks are deferred (exact)
   const DevTables* tabs;
 };
@@ -504,15 +507,27 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   }
 
   // Work distribution.  Static: wave w owns the run [w*per, (w+1)*per) (or round-robin single items).
-  // Dynamic ("guided"): a wave grabs a run of max(1, remaining / (4 * nwaves)) consecutive items with
+  // Dynamic ("guided"): a wave grabs a run of max(1, remaining / (d * nwaves)) consecutive items with
   // ONE atomic, so early runs are long and the tail is single items -- far below the ~88 dequeues/us a
-  // single counter serves.
+  // single counter serves.  d = clamp(total / (64 * nwaves), 4, 32): the first runs are one 64-item descriptor
+  // window.  Measured in one process (diag variants 14-21): d = 4 is best for 128 KiB pieces of 1 MiB blocks
+  // (3a, 3b: d = 8 -1.4 %, 16 -2 %, 32 -4 %; d = 1 or 2 -4 to -8 %), while the Zipf batch (2.1 M items, a third
+  // of them tiny) gains 1.8-2.2 % at d = 16 over d = 4: its item counts say little about bytes, and shorter
+  // runs keep the tail balanced.  The adaptive d is 4 for 3a/3b and 16 for config 4.  Prefetching the next
+  // window's descriptors and the next run's grab a run ahead (so the item stream never drains at a boundary)
+  // was 3.6-8 % SLOWER: the boundaries are not where the time goes, the spread of the waves over the batch is.
   uint64_t lo = ~uint64_t(0), hi = 0;
   uint64_t seen = 0;  // dynamic: counter value this wave last observed
+  uint64_t gdiv = a.guided_div;
+  if (!gdiv) {
+    gdiv = total / (64 * nwaves);
+    gdiv = gdiv < 4 ? 4 : gdiv > 32 ? 32 : gdiv;
+  }
   auto grab = [&]() -> bool {
     if (kDynamic) {
       const uint64_t rem = total > seen ? total - seen : 0;
-      uint64_t c = rem / (4 * nwaves);
+      uint64_t c = rem / (gdiv * nwaves);
+      if (a.guided_cap && c > a.guided_cap) c = a.guided_cap;
       if (c < 1) c = 1;
       if (c > 0xffffffffull) c = 0xffffffffull;
       uint32_t t = 0;
@@ -538,13 +553,12 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   uint64_t w0 = 0, wn = 0;        // window [w0, w0 + wn) of the current run
   uintptr_t w_ps = 0, w_pe = 0;   // per lane
   uint32_t w_b = 0, w_reg0 = 0, w_only = 0;
-  auto fill = [&](uint64_t start, uint64_t stop) {
-    w0 = start;
-    wn = stop - start < 64 ? stop - start : 64;
+  auto fill_set = [&](uint64_t start, uint64_t n, uintptr_t& w_ps, uintptr_t& w_pe, uint32_t& w_b, uint32_t& w_reg0,
+                      uint32_t& w_only) {
     const uint64_t g = start + lane;
     w_ps = w_pe = 0;
     w_b = w_reg0 = w_only = 0;
-    if (g < start + wn) {
+    if (g < start + n) {
       uint64_t b, rs, re;
       bool first, only;
       if (planned) {
@@ -569,6 +583,11 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
       w_reg0 = first ? ~(a.init ? a.init[b] : 0u) : 0u;
       w_only = only ? 1u : 0u;
     }
+  };
+  auto fill = [&](uint64_t start, uint64_t stop) {
+    w0 = start;
+    wn = stop - start < 64 ? stop - start : 64;
+    fill_set(w0, wn, w_ps, w_pe, w_b, w_reg0, w_only);
   };
   struct Item {
     uint64_t g, b;
@@ -1353,6 +1372,20 @@ void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs
     case 10: crc32c_pieces_kernel<P, D, 4, true, true, 0, T, false><<<grid, T, 0, s>>>(a); break;  // 16-B rows
     case 11: crc32c_pieces_kernel<P, D, 4, true, true, 3, T><<<grid, T, 0, s>>>(a); break;  // ablation: no head/tail
     case 12: crc32c_pieces_kernel<P, D, 4, true, true, 4, T><<<grid, T, 0, s>>>(a); break;  // ablation: no lane tree
+    case 14:  // guided grabs of remaining / (d nwaves), d = 1, 2, 8, 16, 32, 4 (default: adaptive)
+    case 15:
+    case 17:
+    case 18:
+    case 19:
+    case 20:  // divisor 4 (the fixed divisor before the adaptive one)
+    case 21: {  // divisor 4, at most 64 items per grab
+      PiecesArgs b = a;
+      b.guided_div = variant == 14 ? 1 : variant == 15 ? 2 : variant == 17 ? 8 : variant == 18 ? 16 : variant == 19 ? 32
+                     : 4;
+      b.guided_cap = variant == 21 ? 64 : 0;
+      crc32c_pieces_kernel<P, D, 4, true, true, 0, T><<<grid, T, 0, s>>>(b);
+      break;
+    }
 #endif
     default: crc32c_pieces_kernel<P, D, 4, true, true, 0, T><<<grid, T, 0, s>>>(a); break;
   }
@@ -1446,6 +1479,8 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
   const uint64_t nwaves_est = uint64_t(c->num_cus) * (kWgThreads / 64);
   const bool dyn = c->dynamic < 0 ? (planned && est_items >= 8 * nwaves_est) : c->dynamic == 1;
   a.static_contig = c->static_contig;
+  a.guided_div = 0;  // adaptive (crc32c_pieces_kernel)
+  a.guided_cap = 0;
   if (dyn) {
     if (!sc.d_counter) KVSEP_HIP(hipMalloc(&sc.d_counter, 16));
     a.work_counter = sc.d_counter;
