@@ -1500,7 +1500,11 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     // (1 GiB of 4 KiB blocks: +5 %; 32 Ki x 16 KiB +2 %, 32 Ki x 32 KiB +6 %).  The 8-wave kernel overlaps the
     // LDS fill with the first group's loads (9; +0.3-2 % over 2); at 16 waves that overlap measured -5 %.
     // 2: always 8 waves; 3: 12 waves; 4 / 5: 8-row groups at 8 / 12 waves; 6: always 16 waves; 7: as 1; 9: 8 waves, fill overlapped with the first loads.
-    const bool eight_waves = max_len <= 8 * 1024 ? count >= (1u << 17) : count >= (1u << 15);
+    // Ragged batches (the max_len hint above 1.25x the mean length total_bytes / count) stay on 16 waves at any
+    // count: their groups wait for their longest block, and more waves hide more of that (Zipf 32 B-32 KiB x 902 K
+    // blocks: 0.93 vs 1.24 ms; lengths uniform in [1, 8 KiB] x 256 K: 4.7 vs 4.0 TB/s).
+    const bool ragged = total_bytes != 0 && 4 * max_len > 5 * (total_bytes / count);
+    const bool eight_waves = !ragged && (max_len <= 8 * 1024 ? count >= (1u << 17) : count >= (1u << 15));
     int nv = c->kernel == 3 ? 6 : c->kernel == 4 ? 9 : (eight_waves ? 9 : 6);
 #ifdef KVSEP_DIAG
     if (c->narrow != 1 && c->narrow != 7 && c->kernel < 3) nv = c->narrow;

@@ -30,6 +30,12 @@ def layout(cfg):
         m = re.fullmatch(r"u(\d+)x(\d+)(?:s(\d+))?(?:f(\d+))?", cfg)
         count, length, stride, first = m.groups()
         return W.uniform_layout(int(count), int(length), int(stride) if stride else None, int(first or 0))
+    if cfg.startswith("r"):  # "r<count>x<max>": ragged, lengths uniform in [1, max], packed
+        count, mx = (int(x) for x in cfg[1:].split("x"))
+        ln = np.random.default_rng(3).integers(1, mx + 1, count).astype(np.uint64)
+        off = np.zeros(count, np.uint64)
+        off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+        return off, ln
     if cfg == "4s":  # config 4's blocks of <= 32 KiB only (86 % of its blocks, 1 % of its bytes)
         off, ln = W.cfg4_layout()
         return off[ln <= 32768], ln[ln <= 32768]
