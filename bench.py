@@ -436,7 +436,7 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     value = total_useful * args.steps / GIB / elapsed
     kern_avg_ms = kern_ms / max(1, launches)
-    kernel_name = ctx.kernel_name(count, max_len)
+    kernel_name = ctx.kernel_name(count, max_len, useful)
     achieved_gbps = useful / (kern_avg_ms * 1e-3) / 1e9
 
     # ---- outside the timed region: u32 results of every rank gathered (RCCL), every block checked

@@ -63,9 +63,10 @@ int kvsep_crc32c_ctx_set_piece_bytes(kvsep_crc32c_ctx* ctx, uint64_t piece_bytes
 /* 0 = static contiguous runs of work items per wave, 2 = static round-robin items, 1 = guided dynamic (one atomic
  * per run of items), -1 = auto (default): guided when long blocks are split into pieces, else static. */
 int kvsep_crc32c_ctx_set_schedule(kvsep_crc32c_ctx* ctx, int dynamic);
-/* Kernel of unsplit batches: 0 = auto (default; the narrow kernel for many blocks <= 8-32 KiB), 1 = always the wide
- * kernel, 2 = the narrow kernel whenever max_len <= 64 KiB, 3 / 4 = as 2 with 16- / 8-wave workgroups.  A choice
- * of speed only: every kernel is exact for every block.  No environment variable changes it. */
+/* Kernel of unsplit batches: 0 = auto (default; the narrow kernel for many blocks <= 8-32 KiB, its sorted-window
+ * form when the batch is ragged: max_len > 1.25 x total_bytes / count), 1 = always the wide kernel, 2 = the narrow
+ * kernel whenever max_len <= 64 KiB, 3 / 4 = as 2 with 16- / 8-wave workgroups, 5 = as 2 in the sorted-window form.
+ * A choice of speed only: every kernel is exact for every block.  No environment variable changes it. */
 int kvsep_crc32c_ctx_set_kernel(kvsep_crc32c_ctx* ctx, int kernel);
 /* Pre-size scratch so later calls of up to `count` blocks / `total_bytes` bytes do not allocate
  * (required before graph capture; covers the planned, narrow, verify and SST-verify forms). */
@@ -73,9 +74,10 @@ int kvsep_crc32c_reserve(kvsep_crc32c_ctx* ctx, uint64_t count, uint64_t total_b
 /* Kernel timing with HIP events on the caller's stream, around the main CRC kernel only. */
 int kvsep_crc32c_ctx_set_timing(kvsep_crc32c_ctx* ctx, int enable);
 int kvsep_crc32c_ctx_get_timing(kvsep_crc32c_ctx* ctx, double* total_ms, uint64_t* launches); /* syncs + resets */
-/* Name of the main kernel a batch of `count` blocks with this max_len hint runs on ("crc32c_pieces_kernel" or
- * "crc32c_narrow_kernel"): the kernel the timing above and a rocprofv3 trace refer to. */
-const char* kvsep_crc32c_kernel_name(kvsep_crc32c_ctx* ctx, uint64_t count, uint64_t max_len);
+/* Name of the main kernel a batch of `count` blocks with these total_bytes / max_len hints runs on
+ * ("crc32c_pieces_kernel", "crc32c_narrow_kernel" or "crc32c_narrow_sorted_kernel"): the kernel the timing above
+ * and a rocprofv3 trace refer to. */
+const char* kvsep_crc32c_kernel_name(kvsep_crc32c_ctx* ctx, uint64_t count, uint64_t total_bytes, uint64_t max_len);
 
 /* ---------------------------------------------------------------- batched device form
  * out[i] = Extend(init ? init[i] : 0, base + off[i], len[i]) for i < count.

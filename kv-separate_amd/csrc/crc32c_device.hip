@@ -861,6 +861,77 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
   return reg;
 }
 
+// Blocks longer than the narrow kernel's hint (a.hint), skipped by the main pass: the wave walks its run
+// [lo, hi) again and checksums those blocks one at a time, each cut into parts of <= 1 GiB, 8 at a time (one per
+// slot; the slot geometry is 32-bit), merged with R(A||B) = Z_|B|(R(A)) ^ R(B) through gf2_shift.  Slower than the
+// main path (long blocks are not what the narrow kernels are for) but exact for any 64-bit length.
+template <int kG, bool kNT, bool kAlignN>
+__device__ __forceinline__ void narrow_deferred(const PiecesArgs& a, const uint8_t* lds, uint64_t lo, uint64_t hi,
+                                                uint32_t lane, uint32_t lc0, uint32_t lc1, uintptr_t dummy) {
+  constexpr uint32_t kPerGroup = 64 / kNarrowLanes;
+  const uint32_t j = lane & (kNarrowLanes - 1);
+  const uint32_t slot = lane / kNarrowLanes;
+  const uint32_t hint32 = uint32_t(a.hint);
+  struct Desc {
+    uint64_t off;
+    uint32_t len, lenhi, init;
+  };
+  auto load_desc = [&](uint64_t g, Desc& d) {
+    const uint64_t b = g + slot;
+    const uint64_t bb = b < hi ? b : hi - 1;
+    d.off = a.off[bb];
+    const uint2 l = *reinterpret_cast<const uint2*>(a.len + bb);
+    d.len = l.x;
+    d.lenhi = l.y;
+    d.init = *(a.init ? a.init + bb : &a.tabs->z4[0][0]);
+  };
+  {
+    for (uint64_t g = lo; g < hi; g += kPerGroup) {
+      Desc d;
+      load_desc(g, d);
+      uint64_t over = __builtin_amdgcn_ballot_w64(g + slot < hi && (d.lenhi != 0 || d.len > hint32));
+      while (over) {
+        const uint32_t k = uint32_t(__builtin_ctzll(over)) / kNarrowLanes;  // slot of the next deferred block
+        over &= ~(0xffull << (k * kNarrowLanes));
+        const uint32_t src = k * kNarrowLanes;
+        const uint64_t boff = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(d.off >> 32)), int(src)))) << 32) |
+                              uint32_t(__builtin_amdgcn_readlane(int(uint32_t(d.off)), int(src)));
+        const uint64_t L = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(d.lenhi), int(src)))) << 32) |
+                           uint32_t(__builtin_amdgcn_readlane(int(d.len), int(src)));
+        const uint32_t binit = uint32_t(__builtin_amdgcn_readlane(int(d.init), int(src)));
+        // parts of q <= 1 GiB bytes (the slot geometry is 32-bit), 8 at a time, one per slot; part p's raw register
+        // (from ~init for part 0, from 0 for the others) is carried to the block's end and the parts XORed
+        uint64_t q = (L + kPerGroup - 1) / kPerGroup;
+        if (q > (1ull << 30)) q = 1ull << 30;
+        const uint64_t nparts = (L + q - 1) / q;
+        const uintptr_t blk = reinterpret_cast<uintptr_t>(a.base) + boff;
+        uint32_t acc = 0;
+        for (uint64_t p0 = 0; p0 < nparts; p0 += kPerGroup) {
+          const uint64_t p = p0 + slot;
+          const uint64_t rs = p < nparts ? p * q : L;
+          const uint64_t re = rs + q < L ? rs + q : L;
+          NStaged<kG> X;
+          nstage<kG, kNT, kAlignN>(X, blk + rs, uint32_t(re - rs), j, dummy);
+          uint32_t km = 0, kn = ~0u;
+#pragma unroll
+          for (uint32_t t = 0; t < kPerGroup; ++t) {
+            const uint32_t kk = uint32_t(__builtin_amdgcn_readlane(int(X.K), int(t * kNarrowLanes)));
+            km = km > kk ? km : kk;
+            kn = kn < kk ? kn : kk;
+          }
+          uint32_t reg = nfinish<kG, kNT, 0, kAlignN>(lds, X, p == 0 ? ~binit : 0u, j, lc0, lc1, kn, km, dummy,
+                                                      NoMid());
+          if (j == kNarrowLanes - 1) reg = gf2_shift(a.tabs, reg, L - re);  // carried to the block's end
+#pragma unroll
+          for (uint32_t t = 0; t < kPerGroup; ++t)
+            acc ^= uint32_t(__builtin_amdgcn_readlane(int(reg), int(t * kNarrowLanes + kNarrowLanes - 1)));
+        }
+        if (lane == 0) emit_block(a, g + k, ~acc);
+      }
+    }
+  }
+}
+
 // Unsplit batches only (every block <= 64 KiB <= piece_bytes); static contiguous runs of 8-block groups.
 template <int kG, bool kNT, int kThreads, bool kOverlap = false, int kAbl = 0, bool kAlignN = true>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
@@ -1006,54 +1077,167 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   KVSEP_NSTAMP(7);
 #undef KVSEP_NSTEP
 #undef KVSEP_NSTAMP
-  if (deferred) {
-    // Blocks longer than the hint: the wave walks its run again and checksums those blocks one at a time, each
-    // cut into 8 contiguous sub-ranges, one per slot (full 64-bit length), merged with R(A||B) = Z_|B|(R(A)) ^ R(B)
-    // through gf2_shift.  Slower than the main path (long blocks are not what this kernel is for) but exact.
-    for (uint64_t g = lo; g < hi; g += kPerGroup) {
-      Desc d;
-      load_desc(g, d);
-      uint64_t over = __builtin_amdgcn_ballot_w64(g + slot < hi && (d.lenhi != 0 || d.len > hint32));
-      while (over) {
-        const uint32_t k = uint32_t(__builtin_ctzll(over)) / kNarrowLanes;  // slot of the next deferred block
-        over &= ~(0xffull << (k * kNarrowLanes));
-        const uint32_t src = k * kNarrowLanes;
-        const uint64_t boff = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(d.off >> 32)), int(src)))) << 32) |
-                              uint32_t(__builtin_amdgcn_readlane(int(uint32_t(d.off)), int(src)));
-        const uint64_t L = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(d.lenhi), int(src)))) << 32) |
-                           uint32_t(__builtin_amdgcn_readlane(int(d.len), int(src)));
-        const uint32_t binit = uint32_t(__builtin_amdgcn_readlane(int(d.init), int(src)));
-        // parts of q <= 1 GiB bytes (the slot geometry is 32-bit), 8 at a time, one per slot; part p's raw register
-        // (from ~init for part 0, from 0 for the others) is carried to the block's end and the parts XORed
-        uint64_t q = (L + kPerGroup - 1) / kPerGroup;
-        if (q > (1ull << 30)) q = 1ull << 30;
-        const uint64_t nparts = (L + q - 1) / q;
-        const uintptr_t blk = reinterpret_cast<uintptr_t>(a.base) + boff;
-        uint32_t acc = 0;
-        for (uint64_t p0 = 0; p0 < nparts; p0 += kPerGroup) {
-          const uint64_t p = p0 + slot;
-          const uint64_t rs = p < nparts ? p * q : L;
-          const uint64_t re = rs + q < L ? rs + q : L;
-          NStaged<kG> X;
-          nstage<kG, kNT, kAlignN>(X, blk + rs, uint32_t(re - rs), j, dummy);
-          uint32_t km = 0, kn = ~0u;
+  if (deferred) narrow_deferred<kG, kNT, kAlignN>(a, lds, lo, hi, lane, lc0, lc1, dummy);
+}
+
+// Bitonic sort of one (key, idx) pair per lane over the wavefront, ascending by key (ties by idx, so the two
+// lanes of every compare-exchange agree): 21 ds_bpermute stages of two values each.
+__device__ __forceinline__ void wave_sort64(uint32_t& key, uint32_t& idx, uint32_t lane) {
+  asm volatile("" : "+v"(lane));  // opaque: keeps the 21 stages' lane ^ j addresses from being hoisted as constants
 #pragma unroll
-          for (uint32_t t = 0; t < kPerGroup; ++t) {
-            const uint32_t kk = uint32_t(__builtin_amdgcn_readlane(int(X.K), int(t * kNarrowLanes)));
-            km = km > kk ? km : kk;
-            kn = kn < kk ? kn : kk;
-          }
-          uint32_t reg = nfinish<kG, kNT, 0, kAlignN>(lds, X, p == 0 ? ~binit : 0u, j, lc0, lc1, kn, km, dummy,
-                                                      NoMid());
-          if (j == kNarrowLanes - 1) reg = gf2_shift(a.tabs, reg, L - re);  // carried to the block's end
+  for (uint32_t k = 2; k <= 64; k <<= 1) {
 #pragma unroll
-          for (uint32_t t = 0; t < kPerGroup; ++t)
-            acc ^= uint32_t(__builtin_amdgcn_readlane(int(reg), int(t * kNarrowLanes + kNarrowLanes - 1)));
-        }
-        if (lane == 0) emit_block(a, g + k, ~acc);
-      }
+    for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+      const int addr = int((lane ^ jj) << 2);
+      const uint32_t pk = uint32_t(__builtin_amdgcn_ds_bpermute(addr, int(key)));
+      const uint32_t pi = uint32_t(__builtin_amdgcn_ds_bpermute(addr, int(idx)));
+      const bool up = (lane & k) == 0;  // this lane's bitonic block sorts ascending
+      const bool low = (lane & jj) == 0;
+      const bool pless = pk < key || (pk == key && pi < idx);
+      const bool take = (low == up) ? pless : !pless;  // the low lane of an ascending pair keeps the minimum
+      key = take ? pk : key;
+      idx = take ? pi : idx;
     }
   }
+}
+
+// Ragged batches of short blocks (see launch_batch_in): the narrow kernel's 8-block groups, but formed from 64-block
+// windows sorted by length, so a group's 8 blocks are of similar length and its slots do not wait for one long
+// block.  Lane i holds the descriptor of block W + i of window W (loaded a window ahead); after the sort, group k's
+// slot s takes the block at sorted position 8k + s (two ds_bpermutes to find it, four to fetch its descriptor).
+// The rows, the slot tree and the end path are the narrow kernel's (nstage / nfinish); blocks over the hint go to
+// narrow_deferred as there.
+template <int kG, bool kNT, int kThreads>
+__global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesArgs a) {
+  constexpr uint32_t kWavesPerWg = kThreads / 64;
+  constexpr uint32_t kPerGroup = 64 / kNarrowLanes;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63u;
+  const uint32_t j = lane & (kNarrowLanes - 1);
+  const uint32_t slot = lane / kNarrowLanes;
+  const uint32_t lc0 = (lane & 31u) << 2;
+  const uint32_t lc1 = lc0 | 0x10000u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerWg;
+  const uintptr_t dummy = reinterpret_cast<uintptr_t>(a.tabs);
+  const uint64_t groups = (a.count + kPerGroup - 1) / kPerGroup;
+  const uint64_t gper = (groups + nwaves - 1) / nwaves;
+  const uint64_t lo = (uint64_t(wave) * gridDim.x + blockIdx.x) * gper * kPerGroup;  // wave-major runs
+  uint64_t hi = lo + gper * kPerGroup;
+  if (hi > a.count) hi = a.count;
+  const uint32_t hint32 = uint32_t(a.hint);  // <= 64 KiB (use_narrow)
+  // window descriptor of block W + lane; len: the length, kOver (longer than the hint: deferred) or kPast (past hi)
+  constexpr uint32_t kOver = 0xffffffffu, kPast = 0xfffffffeu;
+  struct WDesc {  // (the initial register is loaded per group, a group ahead of its use: two VGPRs less)
+    uint64_t off;
+    uint32_t len, idx;  // idx: after the sort, the window lane holding sorted position `lane`
+  };
+  auto load_win = [&](uint64_t W, WDesc& d) {
+    const uint64_t b = W + lane;
+    const bool in = b < hi;
+    const uint64_t bb = in ? b : hi - 1;
+    d.off = a.off[bb];
+    const uint2 l = *reinterpret_cast<const uint2*>(a.len + bb);
+    d.len = !in ? kPast : (l.y != 0 || l.x > hint32) ? kOver : l.x;
+  };
+  auto sort_win = [&](WDesc& d) {
+    uint32_t key = d.len == kOver ? 0u : d.len;  // deferred blocks are empty in this pass: they sort first
+    d.idx = lane;
+    wave_sort64(key, d.idx, lane);
+  };
+  struct NItem {
+    uint64_t w;    // window base (wave-uniform)
+    uint32_t src;  // this lane's slot's block: w + src
+    uint32_t reg0, kmin, kmax;
+    bool live;
+  };
+  bool deferred = false;
+  auto take = [&](uint64_t W, const WDesc& d, uint32_t k, NItem& it, NStaged<kG>& st) {
+    uint32_t sl = slot;
+    asm volatile("" : "+v"(sl));  // see load_desc in crc32c_narrow_kernel
+    const uint32_t src = uint32_t(__builtin_amdgcn_ds_bpermute(int((k * kPerGroup + sl) << 2), int(d.idx)));
+    const int sa = int(src << 2);
+    const uint32_t len = uint32_t(__builtin_amdgcn_ds_bpermute(sa, int(d.len)));
+    const uint32_t offl = uint32_t(__builtin_amdgcn_ds_bpermute(sa, int(uint32_t(d.off))));
+    const uint32_t offh = uint32_t(__builtin_amdgcn_ds_bpermute(sa, int(uint32_t(d.off >> 32))));
+    deferred |= __builtin_amdgcn_ballot_w64(len == kOver) != 0;
+    it.live = len < kPast;
+    it.w = W;
+    it.src = src;
+    it.reg0 = ~*(a.init && it.live ? a.init + (W + src) : &a.tabs->z4[0][0]);  // z4[0][0] == 0
+    const uintptr_t ps = it.live ? reinterpret_cast<uintptr_t>(a.base) + ((uint64_t(offh) << 32) | offl) : dummy;
+    nstage<kG, kNT, true>(st, ps, it.live ? len : 0u, j, dummy);
+    uint32_t km = 0, kn = ~0u;
+#pragma unroll
+    for (uint32_t t = 0; t < kPerGroup; ++t) {
+      const uint32_t kk = uint32_t(__builtin_amdgcn_readlane(int(st.K), int(t * kNarrowLanes)));
+      km = km > kk ? km : kk;
+      kn = kn < kk ? kn : kk;
+    }
+    it.kmax = km;
+    it.kmin = kn;
+  };
+
+  auto take_empty = [&](NItem& it, NStaged<kG>& st) {  // past the last group: the same loads, all to `dummy`
+    it.live = false;
+    it.w = 0;
+    it.src = 0;
+    it.reg0 = 0;
+    uintptr_t d = dummy;
+    asm volatile("" : "+s"(d));  // opaque: its loop-invariant addresses would otherwise be hoisted (and spilled)
+    nstage<kG, kNT, true>(st, d, 0u, j, dummy);
+    it.kmax = it.kmin = 0;
+  };
+
+  WDesc cw, nw;
+  if (lo < hi) load_win(lo, cw);  // its round trip overlaps the LDS fill
+  fill_lds<kThreads, true>(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
+  __syncthreads();
+  if (lo < hi) {
+    uint64_t W = lo, Wn = lo + 64;
+    if (Wn < hi) load_win(Wn, nw);
+    sort_win(cw);
+    auto groups_in = [&](uint64_t w) { return uint32_t(((hi - w < 64 ? hi - w : 64) + kPerGroup - 1) / kPerGroup); };
+    uint32_t k = 0, nk = groups_in(W);
+    NItem cur, nxt;
+    NStaged<kG> S, T;
+    take(W, cw, 0, cur, S);
+    // finish group k of window W (staged in ia / A) while the next group -- k + 1 of W, or the first group of the
+    // next window, sorted right there -- is staged into ib / B
+    auto step = [&](NItem& ia, NStaged<kG>& A, NItem& ib, NStaged<kG>& B) -> bool {
+      const bool here = k + 1 < nk;
+      const bool next_win = !here && Wn < hi;
+      const uint32_t reg = nfinish<kG, kNT, 0, true>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy, [&]() {
+        if (here) {
+          take(W, cw, k + 1, ib, B);
+        } else if (next_win) {
+          sort_win(nw);
+          take(Wn, nw, 0, ib, B);
+        } else {
+          take_empty(ib, B);
+        }
+      });
+      if (j == kNarrowLanes - 1 && ia.live) emit_block(a, ia.w + ia.src, ~reg);
+      if (here) {
+        ++k;
+        return true;
+      }
+      if (!next_win) return false;
+      cw = nw;
+      W = Wn;
+      Wn += 64;
+      k = 0;
+      nk = groups_in(W);
+      if (Wn < hi) load_win(Wn, nw);
+      return true;
+    };
+    for (;;) {
+      if (!step(cur, S, nxt, T)) break;
+      if (!step(nxt, T, cur, S)) break;
+    }
+  }
+  if (deferred) narrow_deferred<kG, kNT, true>(a, lds, lo, hi, lane, lc0, lc1, dummy);
 }
 
 // One thread per block: Horner over the block's pieces, R <- Z_piece(R) ^ R_piece.
@@ -1180,7 +1364,7 @@ struct kvsep_crc32c_ctx {
   uint64_t piece_bytes = 128 * 1024;  // best of 32 KiB .. 1 MiB on configs 3a/3b/4
   bool piece_auto = true;             // smaller pieces for small batches (piece_for); off once set explicitly
   int dynamic = -1;  // -1 auto, 0 static, 1 guided
-  int kernel = 0;    // kvsep_crc32c_ctx_set_kernel: 0 auto (use_narrow), 1 wide only, 2-4 narrow when the hint allows
+  int kernel = 0;    // kvsep_crc32c_ctx_set_kernel: 0 auto (use_narrow), 1 wide only, 2-5 narrow when the hint allows
   uint32_t static_contig = 1;  // static schedule: contiguous runs (1) or round-robin items (0, set_schedule(2))
   int variant = 1;   // KVSEP_DIAG builds only: A/B and ablation variants of the wide kernel (launch_pieces_v)
   int narrow = 1;    // KVSEP_DIAG builds only: narrow-kernel variants
@@ -1306,6 +1490,30 @@ int ensure_plan(Scratch& sc, uint64_t piece_bytes, uint64_t count, uint64_t tota
 //   64 KiB blocks never (16 Ki x 64 KiB: wide 6.22 vs 4.88).
 // The thresholds scale with the CU count (256 on MI355X).  kvsep_crc32c_ctx_set_kernel can force either kernel
 // (tests); the choice never changes a result: both are exact for any block, whatever the hint.
+// A ragged batch: the max_len hint above 1.25x the mean length total_bytes / count (0 = unknown: not ragged).
+bool ragged_batch(uint64_t count, uint64_t total_bytes, uint64_t max_len) {
+  return count != 0 && total_bytes != 0 && 4 * max_len > 5 * (total_bytes / count);
+}
+
+// Narrow-kernel form of a batch that use_narrow() put on the narrow kernels: 6 = 16-wave workgroups, 9 = 8-wave
+// workgroups (fill overlapped with the first loads), 20 = sorted windows (crc32c_narrow_sorted_kernel, 16 waves).
+int narrow_form(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes, uint64_t max_len) {
+  if (c->kernel == 3) return 6;
+  if (c->kernel == 4) return 9;
+  if (c->kernel == 5) return 20;
+  // 16-wave workgroups below 128 Ki blocks of <= 8 KiB (32 Ki blocks of 8-32 KiB), 8-wave ones from there on.  A
+  // small batch gives each wave only a couple of 8-block groups, and more waves hide more of the launch/first-load
+  // ramp (256 MiB of 4 KiB blocks: 16 waves +2-5 %); a large one streams better with 8 (1 GiB of 4 KiB blocks:
+  // +5 %; 32 Ki x 16 KiB +2 %, 32 Ki x 32 KiB +6 %).  The 8-wave kernel overlaps the LDS fill with the first
+  // group's loads (+0.3-2 %); at 16 waves that overlap measured -5 %.
+  // Ragged batches take the sorted-window kernel at any size: an 8-block group waits for its longest block, and
+  // sorting 64-block windows by length makes the groups even (config 4's 902 K blocks <= 32 KiB: 0.93 -> 0.57 ms
+  // against the 16-wave narrow kernel, 1.24 ms on the 8-wave one).
+  if (ragged_batch(count, total_bytes, max_len)) return 20;
+  const bool eight_waves = max_len <= 8 * 1024 ? count >= (1u << 17) : count >= (1u << 15);
+  return eight_waves ? 9 : 6;
+}
+
 bool use_narrow(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t max_len) {
   if (max_len == 0 || max_len > 2 * kNarrowMax) return false;
   if (c->kernel == 1) return false;
@@ -1494,19 +1702,11 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     if (e0 && e1) KVSEP_HIP(hipEventRecord(e0, s));
   }
   if (!planned && use_narrow(c, count, max_len)) {
-    // 1 (default): 16-wave workgroups below 128 Ki blocks of <= 8 KiB (32 Ki blocks of 8-32 KiB), 8-wave ones
-    // from there on.  A small batch gives each wave only a couple of 8-block groups, and more waves hide more of
-    // the launch/first-load ramp (256 MiB of 4 KiB blocks: 16 waves +2-5 %); a large one streams better with 8
-    // (1 GiB of 4 KiB blocks: +5 %; 32 Ki x 16 KiB +2 %, 32 Ki x 32 KiB +6 %).  The 8-wave kernel overlaps the
-    // LDS fill with the first group's loads (9; +0.3-2 % over 2); at 16 waves that overlap measured -5 %.
-    // 2: always 8 waves; 3: 12 waves; 4 / 5: 8-row groups at 8 / 12 waves; 6: always 16 waves; 7: as 1; 9: 8 waves, fill overlapped with the first loads.
-    // Ragged batches (the max_len hint above 1.25x the mean length total_bytes / count) stay on 16 waves at any
-    // count: their groups wait for their longest block, and more waves hide more of that (Zipf 32 B-32 KiB x 902 K
-    // blocks: 0.93 vs 1.24 ms; lengths uniform in [1, 8 KiB] x 256 K: 4.7 vs 4.0 TB/s).
-    const bool ragged = total_bytes != 0 && 4 * max_len > 5 * (total_bytes / count);
-    const bool eight_waves = !ragged && (max_len <= 8 * 1024 ? count >= (1u << 17) : count >= (1u << 15));
-    int nv = c->kernel == 3 ? 6 : c->kernel == 4 ? 9 : (eight_waves ? 9 : 6);
+    int nv = narrow_form(c, count, total_bytes, max_len);
 #ifdef KVSEP_DIAG
+    // diag narrow variants: 2: always 8 waves; 3: 12 waves; 4 / 5: 8-row groups at 8 / 12 waves; 6: always 16
+    // waves; 7: as 1; 9: 8 waves, fill overlapped with the first loads; 20 / 21 / 22: sorted windows at 16 / 8 / 12
+    // waves; 12, 14, 16-19: see the cases below
     if (c->narrow != 1 && c->narrow != 7 && c->kernel < 3) nv = c->narrow;
 #endif
     a.hint = max_len;
@@ -1522,8 +1722,11 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
       case 18: crc32c_narrow_kernel<4, true, 1024, false, 0, false><<<grid, 1024, 0, s>>>(a); break;  // 16-B rows
       case 19: crc32c_narrow_kernel<4, true, 512, true, 0, false><<<grid, 512, 0, s>>>(a); break;     // 16-B rows
       case 17: crc32c_narrow_kernel<4, true, 512, true, 1><<<grid, 512, 0, s>>>(a); break;    // ablation
+      case 21: crc32c_narrow_sorted_kernel<4, true, 512><<<grid, 512, 0, s>>>(a); break;
+      case 22: crc32c_narrow_sorted_kernel<4, true, 768><<<grid, 768, 0, s>>>(a); break;
 #endif
       case 9: crc32c_narrow_kernel<4, true, 512, true><<<grid, 512, 0, s>>>(a); break;
+      case 20: crc32c_narrow_sorted_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
       default: crc32c_narrow_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
     }
   } else {
@@ -1639,7 +1842,7 @@ int kvsep_crc32c_ctx_set_schedule(kvsep_crc32c_ctx* c, int dynamic) {
 }
 
 int kvsep_crc32c_ctx_set_kernel(kvsep_crc32c_ctx* c, int kernel) {
-  if (!c || kernel < 0 || kernel > 4) return set_err(KVSEP_EINVAL, "kernel must be 0..4");
+  if (!c || kernel < 0 || kernel > 5) return set_err(KVSEP_EINVAL, "kernel must be 0..5");
   std::lock_guard<std::mutex> g(c->mu);
   c->kernel = kernel;
   return KVSEP_OK;
@@ -1769,10 +1972,11 @@ int kvsep_sst_verify_device(kvsep_crc32c_ctx* c, void* stream, const void* file_
   return capturing ? KVSEP_OK : release(sc, s);
 }
 
-const char* kvsep_crc32c_kernel_name(kvsep_crc32c_ctx* c, uint64_t count, uint64_t max_len) {
+const char* kvsep_crc32c_kernel_name(kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes, uint64_t max_len) {
   if (!c) return "";
   const bool planned = !(max_len != 0 && max_len <= c->piece_bytes);
-  return !planned && use_narrow(c, count, max_len) ? "crc32c_narrow_kernel" : "crc32c_pieces_kernel";
+  if (planned || !use_narrow(c, count, max_len)) return "crc32c_pieces_kernel";
+  return narrow_form(c, count, total_bytes, max_len) == 20 ? "crc32c_narrow_sorted_kernel" : "crc32c_narrow_kernel";
 }
 
 int kvsep_stream_read_device(kvsep_crc32c_ctx* c, void* stream, const void* src, uint64_t nbytes, uint32_t* sink) {

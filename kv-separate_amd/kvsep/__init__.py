@@ -51,7 +51,7 @@ _SIGS = {
     "kvsep_accelerated_crc32c": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
     "kvsep_set_offload_threshold": (None, [ctypes.c_uint64]),
     "kvsep_offload_stats": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
-    "kvsep_crc32c_kernel_name": (ctypes.c_char_p, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]),
+    "kvsep_crc32c_kernel_name": (ctypes.c_char_p, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]),
     "kvsep_crc32c_extend_host": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
     "kvsep_crc32c_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "kvsep_crc32c_ctx_destroy": (None, [ctypes.c_void_p]),
@@ -253,20 +253,20 @@ class Context:
         v = -1 if dynamic is None else 2 if dynamic == "rr" else (1 if dynamic else 0)
         _check(lib().kvsep_crc32c_ctx_set_schedule(self._h, v), "set_schedule")
 
-    KERNELS = {"auto": 0, "wide": 1, "narrow": 2, "narrow16": 3, "narrow8": 4}
+    KERNELS = {"auto": 0, "wide": 1, "narrow": 2, "narrow16": 3, "narrow8": 4, "sorted": 5}
 
     def set_kernel(self, kernel: str):
         """Kernel choice for unsplit batches (kvsep_crc32c_ctx_set_kernel): "auto" (default), "wide", or the narrow
-        kernel whenever the max_len hint is <= 64 KiB ("narrow"; "narrow16" / "narrow8" pin its workgroup size).
-        Never changes a result."""
+        kernel whenever the max_len hint is <= 64 KiB ("narrow"; "narrow16" / "narrow8" pin its workgroup size,
+        "sorted" its sorted-window form for ragged batches).  Never changes a result."""
         _check(lib().kvsep_crc32c_ctx_set_kernel(self._h, self.KERNELS[kernel]), "set_kernel")
 
     def reserve(self, count: int, total_bytes: int):
         _check(lib().kvsep_crc32c_reserve(self._h, count, total_bytes), "reserve")
 
-    def kernel_name(self, count: int, max_len: int) -> str:
-        """The main kernel a batch of `count` blocks with this max_len hint runs on."""
-        return lib().kvsep_crc32c_kernel_name(self._h, count, max_len).decode()
+    def kernel_name(self, count: int, max_len: int, total_bytes: int = 0) -> str:
+        """The main kernel a batch of `count` blocks with these max_len / total_bytes hints runs on."""
+        return lib().kvsep_crc32c_kernel_name(self._h, count, total_bytes, max_len).decode()
 
     def set_timing(self, on: bool):
         _check(lib().kvsep_crc32c_ctx_set_timing(self._h, 1 if on else 0), "set_timing")

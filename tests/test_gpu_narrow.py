@@ -114,7 +114,44 @@ def test_verify_mode_narrow(ctxs, oracle, pool):
     assert np.array_equal(out.cpu().numpy().view(np.uint32), crc)
 
 
-@pytest.mark.parametrize("kernel", ["narrow16", "narrow8"])
+@pytest.mark.parametrize("count", [1, 63, 64, 65, 200, 5000])
+def test_sorted_windows_ragged(oracle, pool, count):
+    """The sorted-window form (crc32c_narrow_sorted_kernel): Zipf-like lengths, partial windows, empty blocks, blocks
+    over the hint (deferred), any alignment, random inits; batch and verify forms; and that auto routing picks it
+    for a ragged batch and keeps the plain narrow kernel for a uniform one."""
+    data, d = pool
+    rng = np.random.default_rng(count + 7)
+    ln = np.minimum((32 * 2.0 ** rng.integers(0, 11, count)) * rng.random(count), 40000).astype(np.uint64)
+    ln[rng.random(count) < 0.05] = 0
+    off = rng.integers(0, data.size - 40001, count).astype(np.uint64)
+    init = rng.integers(0, 2**32, count, dtype=np.uint64).astype(np.uint32)
+    exp = oracle.batch(data, off, ln, init, threads=8)
+    ctx = kvsep.Context(0)
+    try:
+        ctx.set_kernel("sorted")
+        assert np.array_equal(run(ctx, d, off, ln, init), exp)
+        assert np.array_equal(run(ctx, d, off, ln, init, max_len=2048), exp)  # longer blocks deferred
+        masked = np.array([oracle.lib.oracle_crc32c_mask(int(c)) for c in exp], np.uint32)
+        bad = sorted({0, count // 2, count - 1})
+        masked[bad] ^= 4
+        out = torch.zeros(count, dtype=torch.int32, device=DEV)
+        fb = torch.zeros(1, dtype=torch.int64, device=DEV)
+        nb = torch.zeros(1, dtype=torch.int64, device=DEV)
+        ctx.verify_device(d.data_ptr(), dev_u64(off), dev_u64(ln), dev_u32(masked), out, fb, nb, init=dev_u32(init),
+                          total_bytes=int(ln.sum()), max_len=int(ln.max()))
+        torch.cuda.synchronize()
+        assert (fb.item(), nb.item()) == (bad[0], len(bad))
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), exp)
+        ctx.set_kernel("auto")
+        n = 40000  # enough blocks for the narrow kernels (use_narrow); ragged -> sorted, uniform -> plain
+        assert ctx.kernel_name(n, 32768, n * 2000) == "crc32c_narrow_sorted_kernel"
+        assert ctx.kernel_name(n, 4096, n * 4096) == "crc32c_narrow_kernel"
+        assert ctx.kernel_name(n, 4096) == "crc32c_narrow_kernel"  # total_bytes unknown: not ragged
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted"])
 def test_every_end_geometry(oracle, pool, kernel):
     """Every case of the slot's end path: m = 0..7 whole 16-B chunks between the 128-B grid and the 16-B end (m = 7
     uses all of lanes 0..6 of the tail load), each with head and tail bytes 0..15, with and without body rows."""

@@ -65,7 +65,7 @@ def test_wide_schedules_ragged(ragged, sched):
         ctx.close()
 
 
-@pytest.mark.parametrize("kernel", ["narrow", "narrow16", "narrow8"])
+@pytest.mark.parametrize("kernel", ["narrow", "narrow16", "narrow8", "sorted"])
 def test_narrow_workgroups_ragged(ragged, kernel):
     d, off, ln, init, exp = ragged
     ctx = kvsep.Context(0)
@@ -78,7 +78,7 @@ def test_narrow_workgroups_ragged(ragged, kernel):
         ctx.close()
 
 
-@pytest.mark.parametrize("kernel", ["auto", "wide", "narrow16", "narrow8"])
+@pytest.mark.parametrize("kernel", ["auto", "wide", "narrow16", "narrow8", "sorted"])
 def test_understated_hint_is_exact(ragged, kernel):
     """max_len = 4 KiB although blocks run to 40 KB: blocks over the hint are deferred (narrow) or whole (wide)."""
     d, off, ln, init, exp = ragged
@@ -93,8 +93,9 @@ def test_understated_hint_is_exact(ragged, kernel):
         ctx.close()
 
 
-@pytest.mark.parametrize("n", [(1 << 32) + 77, (9 << 30) + 5])
-def test_understated_hint_block_over_4gib(oracle, n):
+@pytest.mark.parametrize("n,kernel", [((1 << 32) + 77, "narrow16"), ((9 << 30) + 5, "narrow16"),
+                                      ((1 << 32) + 77, "sorted")])
+def test_understated_hint_block_over_4gib(oracle, n, kernel):
     """A 2^32 + 77-byte block among 4 KiB blocks under a 4 KiB hint, on the narrow kernel: its length does not fit
     the narrow kernel's 32-bit staging, so it must take the deferred path with its full 64-bit length.  At 9 GiB + 5
     the deferred path cuts it into 10 parts of <= 1 GiB, two rounds of 8 slots."""
@@ -102,7 +103,7 @@ def test_understated_hint_block_over_4gib(oracle, n):
     kvsep.fill_splitmix64(buf.data_ptr(), buf.numel(), 4242, 0)
     ctx = kvsep.Context(0)
     try:
-        ctx.set_kernel("narrow16")
+        ctx.set_kernel(kernel)
         off = np.concatenate([np.arange(64, dtype=np.uint64) * np.uint64(4096), [np.uint64(4096 * 64 + 3)]])
         ln = np.concatenate([np.full(64, 4096, np.uint64), [np.uint64(n)]])
         got = run(ctx, buf, off, ln, None, max_len=4096, base=buf.data_ptr())
