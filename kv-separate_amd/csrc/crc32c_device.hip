@@ -164,20 +164,23 @@ __device__ __forceinline__ uint4 uniform4(uint4 v) {
 
 // Serial steps over bytes [q0, q1) of a 16-B aligned chunk (0 <= q0 <= q1 <= 16), wave-uniform.
 // Aligned whole words take one Z_4 step (util/crc32c.cc STEP4W), the rest byte steps (STEP1).
-__device__ __forceinline__ uint32_t serial16(const uint8_t* lds, uint32_t reg, uint4 ch, int q0, int q1) {
+// z4 / byte: where the LDS image keeps Z_4 and the STEP1 table (the compact narrow image reads the STEP1 table as
+// Z_4's byte-3 table: Z_4(b << 24) = Z_1(b), see LdsCompact).
+__device__ __forceinline__ uint32_t serial16(const uint8_t* lds, uint32_t reg, uint4 ch, int q0, int q1,
+                                             uint32_t z4 = kZ4Off, uint32_t byte = kByteOff) {
   const uint32_t w[4] = {ch.x, ch.y, ch.z, ch.w};
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int lo = 4 * k;
     if (q0 <= lo && lo + 4 <= q1) {
-      reg = zmap(lds, kZ4Off, reg ^ w[k]);
+      reg = zmap(lds, z4, reg ^ w[k]);
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int pos = lo + i;
         if (pos >= q0 && pos < q1) {
           const uint32_t b = (reg ^ (w[k] >> (8 * i))) & 0xffu;
-          reg = lds_u32(lds, kByteOff + (b << 2)) ^ (reg >> 8);
+          reg = lds_u32(lds, byte + (b << 2)) ^ (reg >> 8);
         }
       }
     }
@@ -473,6 +476,77 @@ __device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* rep, cons
   }
 }
 
+// LDS layouts of the narrow kernels (template parameter Lay of nfinish and the narrow kernel).
+//   LdsFull: the pieces kernel's image (157 KiB; the narrow kernel fills only Z_128 replicated 32x and the small
+//     tables it reads): every lookup conflict-free, one workgroup per CU.
+//   LdsCompact: 80 KiB, so that two workgroups fit one CU: Z_128 replicated 16x at byte b<<8 | k<<6 | copy<<2
+//     (table k, copy = lane % 16), then Z_4 and Z_16 / Z_32 / Z_64; the STEP1 table is read as Z_4's byte-3 table
+//     (Z_4(b << 24) = Z_1(b): three of the four zero bytes only shift b down).  Lanes l and l + 16 of a 32-lane
+//     LDS group share a copy, so a lookup is a 2-way bank conflict (4 LDS-array cycles per wave-instruction, not 2).
+struct LdsFull {
+  static constexpr uint32_t kBytes = kLdsBytes, kZ4 = kZ4Off, kTree = kTreeOff, kByte = kByteOff;
+  static constexpr bool kCompact = false;
+  static __device__ __forceinline__ uint32_t lc0(uint32_t lane) { return (lane & 31u) << 2; }
+  static __device__ __forceinline__ uint32_t lc1(uint32_t lane) { return ((lane & 31u) << 2) | 0x10000u; }
+  static __device__ __forceinline__ uint32_t fold(const uint8_t* lds, uint32_t c, uint32_t w, uint32_t lc0,
+                                                  uint32_t lc1) {
+    return fold_step(lds, c, w, lc0, lc1);
+  }
+};
+struct LdsCompact {
+  static constexpr uint32_t kBytes = 81920, kZ4 = 65536, kTree = 65536 + 4096, kByte = 65536 + 3072;
+  static constexpr bool kCompact = true;
+  static __device__ __forceinline__ uint32_t lc0(uint32_t lane) { return (lane & 15u) << 2; }
+  static __device__ __forceinline__ uint32_t lc1(uint32_t) { return 0; }
+  static __device__ __forceinline__ uint32_t fold(const uint8_t* lds, uint32_t c, uint32_t w, uint32_t lc0,
+                                                  uint32_t) {
+    // v_perm_b32: byte0 = lc0.byte0 (copy*4), byte1 = c.byte k, bytes 2-3 zero; table k by the immediate offset
+    const uint32_t a0 = __builtin_amdgcn_perm(c, lc0, 0x0C0C0400u);
+    const uint32_t a1 = __builtin_amdgcn_perm(c, lc0, 0x0C0C0500u);
+    const uint32_t a2 = __builtin_amdgcn_perm(c, lc0, 0x0C0C0600u);
+    const uint32_t a3 = __builtin_amdgcn_perm(c, lc0, 0x0C0C0700u);
+    return xor3(xor3(lds_u32(lds, a0), lds_u32(lds, a1 + 64u), w), lds_u32(lds, a2 + 128u), lds_u32(lds, a3 + 192u));
+  }
+};
+static_assert(LdsCompact::kTree + 3 * 4096 == LdsCompact::kBytes, "compact narrow image");
+
+// The compact image's fill (LdsCompact): 4096 16-B stores of the replicated Z_128 and the 16 KiB run Z_4, Z_16,
+// Z_32, Z_64 (contiguous in DevTables from z4).  All loads before the first store, `mid()` between (see fill_lds).
+template <int kThreads, typename Mid = NoMid>
+__device__ __forceinline__ void fill_lds_compact(uint8_t* lds, const uint32_t* rep, const DevTables* tabs,
+                                                 uint32_t tid, Mid&& mid = Mid()) {
+  constexpr uint32_t kRep = (4096 + kThreads - 1) / kThreads;
+  constexpr uint32_t kN16 = 4 * 4096 / 16;
+  constexpr uint32_t kSmall = (kN16 + kThreads - 1) / kThreads;
+  uint4* l128 = reinterpret_cast<uint4*>(lds);
+  const uint4* src = reinterpret_cast<const uint4*>(&tabs->z4[0][0]);
+  uint32_t v[kRep];
+  uint4 w[kSmall];
+#pragma unroll
+  for (uint32_t i = 0; i < kRep; ++i) {
+    const uint32_t q = tid + i * kThreads;  // bytes 16q .. 16q+15 = b<<8 | k<<6 | 4 copies
+    v[i] = q < 4096 ? rep[((q >> 2) & 3u) * 256u + (q >> 4)] : 0u;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kSmall; ++i) {
+    const uint32_t q = tid + i * kThreads;
+    w[i] = q < kN16 ? src[q] : make_uint4(0, 0, 0, 0);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  mid();
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (uint32_t i = 0; i < kRep; ++i) {
+    const uint32_t q = tid + i * kThreads;
+    if (q < 4096) l128[q] = make_uint4(v[i], v[i], v[i], v[i]);
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kSmall; ++i) {
+    const uint32_t q = tid + i * kThreads;
+    if (q < kN16) l128[LdsCompact::kZ4 / 16 + q] = w[i];
+  }
+}
+
 // kThreads: 512 (8 waves, 2 per SIMD, <= 256 VGPRs; the default), 768, 1024 or 256 for A/B (launch_pieces_v).
 // One workgroup per CU in every case (the LDS image is 157 KiB).
 template <bool kPlanned, bool kDynamic, int kG, bool kNT, bool kAhead, int kAbl = 0, int kThreads = kWgThreads,
@@ -755,7 +829,7 @@ __device__ __forceinline__ void nstage(NStaged<kG>& s, uintptr_t ps, uint32_t le
 
 // Raw register after the slot item, valid in the slot's last lane (j == 7).  kmin / kmax: wave min / max of K.
 // `next()` stages the following group, after this group's last row loads (see the wide kernel's finish()).
-template <int kG, bool kNT, int kAbl = 0, bool kAlign = true, typename Next>  // kAbl != 0: ablation (wrong)
+template <int kG, bool kNT, int kAbl = 0, bool kAlign = true, typename Lay = LdsFull, typename Next>  // kAbl != 0: ablation (wrong)
 __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, uint32_t reg, uint32_t j,
                                             uint32_t lc0, uint32_t lc1, uint32_t kmin, uint32_t kmax,
                                             uintptr_t dummy, Next&& next) {
@@ -765,7 +839,7 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
   const uint32_t endg = (g.E - g.a1) | (g.a1 - g.ar);
   const int32_t rel0 = int32_t(uint32_t(s.seg) - uint32_t(s.ps) + g.P);  // row 0's chunk from the line (as staged)
   if (!kmax) next();
-  if (g.P < g.h0) reg = serial16(lds, reg, s.hc, int(g.P & 15u), int(g.h0 - (g.P & ~15u)));
+  if (g.P < g.h0) reg = serial16(lds, reg, s.hc, int(g.P & 15u), int(g.h0 - (g.P & ~15u)), Lay::kZ4, Lay::kByte);
   if (kmax) {
     const uint32_t K = s.K, last = K > 1 ? K - 1 : 0;
     uint4 v = (K && rel0 >= int32_t(g.h0)) ? s.v : make_uint4(0, 0, 0, 0);
@@ -776,10 +850,10 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
     if (kAbl) {                                                       \
       c0 ^= (V).x; c1 ^= (V).y; c2 ^= (V).z; c3 ^= (V).w;             \
     } else {                                                          \
-      c0 = fold_step(lds, c0, (V).x, lc0, lc1);                       \
-      c1 = fold_step(lds, c1, (V).y, lc0, lc1);                       \
-      c2 = fold_step(lds, c2, (V).z, lc0, lc1);                       \
-      c3 = fold_step(lds, c3, (V).w, lc0, lc1);                       \
+      c0 = Lay::fold(lds, c0, (V).x, lc0, lc1);                       \
+      c1 = Lay::fold(lds, c1, (V).y, lc0, lc1);                       \
+      c2 = Lay::fold(lds, c2, (V).z, lc0, lc1);                       \
+      c3 = Lay::fold(lds, c3, (V).w, lc0, lc1);                       \
     }                                                                 \
   } while (0)
     uint32_t r = 1;
@@ -811,23 +885,23 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
     for (int i = 0; i < kG; ++i)
       if (r + i < K) KVSEP_NROW(s.A[i]);
 #undef KVSEP_NROW
-    uint32_t p = zmap_x(lds, kZ4Off, c0, c1);
-    p = zmap_x(lds, kZ4Off, p, c2);
-    p = zmap_x(lds, kZ4Off, p, c3);
+    uint32_t p = zmap_x(lds, Lay::kZ4, c0, c1);
+    p = zmap_x(lds, Lay::kZ4, p, c2);
+    p = zmap_x(lds, Lay::kZ4, p, c3);
     // 3-level tree inside the slot (lanes 8k .. 8k+7 of one DPP row): Z_16, Z_32, Z_64
     {
       const uint32_t o = row_shr<1>(p);
-      if ((j & 1u) == 1u) p = zmap_x(lds, kTreeOff, o, p);
+      if ((j & 1u) == 1u) p = zmap_x(lds, Lay::kTree, o, p);
     }
     {
       const uint32_t o = row_shr<2>(p);
-      if ((j & 3u) == 3u) p = zmap_x(lds, kTreeOff + 4096u, o, p);
+      if ((j & 3u) == 3u) p = zmap_x(lds, Lay::kTree + 4096u, o, p);
     }
     {
       const uint32_t o = row_shr<4>(p);
-      if ((j & 7u) == 7u) p = zmap_x(lds, kTreeOff + 8192u, o, p);
+      if ((j & 7u) == 7u) p = zmap_x(lds, Lay::kTree + 8192u, o, p);
     }
-    if (K) reg = zmap(lds, kZ4Off, p);  // lane 7 of the slot: pending word at the rows' end - 4 -> register there
+    if (K) reg = zmap(lds, Lay::kZ4, p);  // lane 7 of the slot: pending word at the rows' end - 4 -> register there
   }
   if (kAlign) {
     const uint32_t m = endg >> 4;
@@ -835,29 +909,29 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
       // their raw register from 0: per lane the STEP4W re-injection, moved up one lane (chunks in lanes 8-m .. 7),
       // the slot's 3-level tree; then R = Z_16m(register at ar) ^ that (Z_16m from the tree tables by the bits of m)
       const uint4 e = j < kNarrowLanes - 1 && j + m >= kNarrowLanes - 1 ? s.tc : make_uint4(0, 0, 0, 0);
-      uint32_t p = zmap_x(lds, kZ4Off, e.x, e.y);
-      p = zmap_x(lds, kZ4Off, p, e.z);
-      p = zmap_x(lds, kZ4Off, p, e.w);
+      uint32_t p = zmap_x(lds, Lay::kZ4, e.x, e.y);
+      p = zmap_x(lds, Lay::kZ4, p, e.z);
+      p = zmap_x(lds, Lay::kZ4, p, e.w);
       p = row_shr<1>(p);  // lane 8k + 7 holds no chunk (its e is zero, so p is zero): slot k+1's lane 0 gets 0
       {
         const uint32_t o = row_shr<1>(p);
-        if ((j & 1u) == 1u) p = zmap_x(lds, kTreeOff, o, p);
+        if ((j & 1u) == 1u) p = zmap_x(lds, Lay::kTree, o, p);
       }
       {
         const uint32_t o = row_shr<2>(p);
-        if ((j & 3u) == 3u) p = zmap_x(lds, kTreeOff + 4096u, o, p);
+        if ((j & 3u) == 3u) p = zmap_x(lds, Lay::kTree + 4096u, o, p);
       }
       {
         const uint32_t o = row_shr<4>(p);
-        if ((j & 7u) == 7u) p = zmap_x(lds, kTreeOff + 8192u, o, p);
+        if ((j & 7u) == 7u) p = zmap_x(lds, Lay::kTree + 8192u, o, p);
       }
-      if (m & 1u) reg = zmap(lds, kTreeOff, reg);
-      if (m & 2u) reg = zmap(lds, kTreeOff + 4096u, reg);
-      if (m & 4u) reg = zmap(lds, kTreeOff + 8192u, reg);
-      reg ^= zmap(lds, kZ4Off, p);  // lane 7: register at a1
+      if (m & 1u) reg = zmap(lds, Lay::kTree, reg);
+      if (m & 2u) reg = zmap(lds, Lay::kTree + 4096u, reg);
+      if (m & 4u) reg = zmap(lds, Lay::kTree + 8192u, reg);
+      reg ^= zmap(lds, Lay::kZ4, p);  // lane 7: register at a1
     }
   }
-  if (endg & 15u) reg = serial16(lds, reg, s.tc, 0, int(endg & 15u));  // lane 7's tail load is the chunk at a1
+  if (endg & 15u) reg = serial16(lds, reg, s.tc, 0, int(endg & 15u), Lay::kZ4, Lay::kByte);  // lane 7's tail load is the chunk at a1
   return reg;
 }
 
@@ -865,7 +939,7 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
 // [lo, hi) again and checksums those blocks one at a time, each cut into parts of <= 1 GiB, 8 at a time (one per
 // slot; the slot geometry is 32-bit), merged with R(A||B) = Z_|B|(R(A)) ^ R(B) through gf2_shift.  Slower than the
 // main path (long blocks are not what the narrow kernels are for) but exact for any 64-bit length.
-template <int kG, bool kNT, bool kAlignN>
+template <int kG, bool kNT, bool kAlignN, typename Lay = LdsFull>
 __device__ __forceinline__ void narrow_deferred(const PiecesArgs& a, const uint8_t* lds, uint64_t lo, uint64_t hi,
                                                 uint32_t lane, uint32_t lc0, uint32_t lc1, uintptr_t dummy) {
   constexpr uint32_t kPerGroup = 64 / kNarrowLanes;
@@ -919,8 +993,8 @@ __device__ __forceinline__ void narrow_deferred(const PiecesArgs& a, const uint8
             km = km > kk ? km : kk;
             kn = kn < kk ? kn : kk;
           }
-          uint32_t reg = nfinish<kG, kNT, 0, kAlignN>(lds, X, p == 0 ? ~binit : 0u, j, lc0, lc1, kn, km, dummy,
-                                                      NoMid());
+          uint32_t reg = nfinish<kG, kNT, 0, kAlignN, Lay>(lds, X, p == 0 ? ~binit : 0u, j, lc0, lc1, kn, km, dummy,
+                                                         NoMid());
           if (j == kNarrowLanes - 1) reg = gf2_shift(a.tabs, reg, L - re);  // carried to the block's end
 #pragma unroll
           for (uint32_t t = 0; t < kPerGroup; ++t)
@@ -933,16 +1007,19 @@ __device__ __forceinline__ void narrow_deferred(const PiecesArgs& a, const uint8
 }
 
 // Unsplit batches only (every block <= 64 KiB <= piece_bytes); static contiguous runs of 8-block groups.
-template <int kG, bool kNT, int kThreads, bool kOverlap = false, int kAbl = 0, bool kAlignN = true>
+// Lay: the LDS layout (LdsFull: one workgroup per CU; LdsCompact: two).  The runs follow gridDim, so a grid of more
+// workgroups than fit at once is the same computation (the hardware dispatcher then hands out the runs).
+template <int kG, bool kNT, int kThreads, bool kOverlap = false, int kAbl = 0, bool kAlignN = true,
+          typename Lay = LdsFull>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[Lay::kBytes];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
   const uint32_t j = lane & (kNarrowLanes - 1);
   const uint32_t slot = lane / kNarrowLanes;
-  const uint32_t lc0 = (lane & 31u) << 2;
-  const uint32_t lc1 = lc0 | 0x10000u;
+  const uint32_t lc0 = Lay::lc0(lane);
+  const uint32_t lc1 = Lay::lc1(lane);
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerWg;
   const uintptr_t dummy = reinterpret_cast<uintptr_t>(a.tabs);
@@ -1013,8 +1090,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     const uint64_t gn = g + kPerGroup;
     // the next group is staged inside nfinish, after this group's last row loads; unconditional (past the
     // end it is an empty group of dummy loads: see the wide kernel's step())
-    const uint32_t reg = nfinish<kG, kNT, kAbl, kAlignN>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
-                                          [&]() { take(gn, ib, B); });
+    const uint32_t reg = nfinish<kG, kNT, kAbl, kAlignN, Lay>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
+                                                           [&]() { take(gn, ib, B); });
     if (j == kNarrowLanes - 1 && g + slot < hi && !ia.over) emit_block(a, g + slot, ~reg);
     load_desc(gn + kPerGroup, dn);  // here, where this group's registers are dead
     return gn < hi;
@@ -1044,14 +1121,17 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     // only, so the first HBM round trip overlaps the fill.  Unconditional (an idle wave stages an empty
     // group), so the store's wait count is the same on every path.
     load_desc(lo, dn);
-    fill_lds<kThreads, true>(lds, &a.tabs->znarrow[0][0], a.tabs, tid, [&]() {
+    auto mid = [&]() {
       take(lo, cur, S);
       load_desc(lo + kPerGroup, dn);
-    });
+    };
+    if constexpr (Lay::kCompact) fill_lds_compact<kThreads>(lds, &a.tabs->znarrow[0][0], a.tabs, tid, mid);
+    else fill_lds<kThreads, true>(lds, &a.tabs->znarrow[0][0], a.tabs, tid, mid);
     __syncthreads();
   } else {
     if (lo < hi) load_desc(lo, dn);
-    fill_lds<kThreads, true>(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
+    if constexpr (Lay::kCompact) fill_lds_compact<kThreads>(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
+    else fill_lds<kThreads, true>(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
     __syncthreads();
     if (lo < hi) {
       take(lo, cur, S);
@@ -1077,7 +1157,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   KVSEP_NSTAMP(7);
 #undef KVSEP_NSTEP
 #undef KVSEP_NSTAMP
-  if (deferred) narrow_deferred<kG, kNT, kAlignN>(a, lds, lo, hi, lane, lc0, lc1, dummy);
+  if (deferred) narrow_deferred<kG, kNT, kAlignN, Lay>(a, lds, lo, hi, lane, lc0, lc1, dummy);
 }
 
 // Bitonic sort of one (key, idx) pair per lane over the wavefront, ascending by key (ties by idx, so the two
@@ -1724,6 +1804,33 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
       case 17: crc32c_narrow_kernel<4, true, 512, true, 1><<<grid, 512, 0, s>>>(a); break;    // ablation
       case 21: crc32c_narrow_sorted_kernel<4, true, 512><<<grid, 512, 0, s>>>(a); break;
       case 22: crc32c_narrow_sorted_kernel<4, true, 768><<<grid, 768, 0, s>>>(a); break;
+      // compact 80 KiB LDS image (two workgroups per CU): 30 / 34: 8-wave workgroups, two per CU, persistent (34:
+      // fill overlapped); 31 / 35: one 8-block group per wave, grid over the whole batch (the dispatcher balances);
+      // 32: two groups per wave; 33: 16-wave workgroups, one per CU (the conflict cost alone)
+      case 30:
+      case 31:
+      case 32:
+      case 34:
+      case 35: {
+        const uint64_t groups = (count + 7) / 8;
+        const uint64_t per = nv == 31 || nv == 35 ? 8 : nv == 32 ? 16 : 0;
+        uint64_t g2 = 2ull * grid;
+        if (per && (groups + per - 1) / per > g2) g2 = (groups + per - 1) / per;
+        if (nv == 34 || nv == 35)
+          crc32c_narrow_kernel<4, true, 512, true, 0, true, LdsCompact><<<unsigned(g2), 512, 0, s>>>(a);
+        else
+          crc32c_narrow_kernel<4, true, 512, false, 0, true, LdsCompact><<<unsigned(g2), 512, 0, s>>>(a);
+        break;
+      }
+      case 33: crc32c_narrow_kernel<4, true, 1024, false, 0, true, LdsCompact><<<grid, 1024, 0, s>>>(a); break;
+      case 36: crc32c_narrow_kernel<2, true, 1024, false, 0, true, LdsCompact><<<grid, 1024, 0, s>>>(a); break;
+      case 37: crc32c_narrow_kernel<2, true, 1024><<<grid, 1024, 0, s>>>(a); break;
+      case 38: crc32c_narrow_kernel<4, true, 1024, true, 0, true, LdsCompact><<<grid, 1024, 0, s>>>(a); break;
+      // one wave per SIMD with deep row groups (no issue-age order between a SIMD's waves): 40 / 41: 4 waves, 16 /
+      // 8-row groups; 42: 4 waves, 16-row groups, fill overlapped (8 waves with 16-row groups spill)
+      case 40: crc32c_narrow_kernel<16, true, 256><<<grid, 256, 0, s>>>(a); break;
+      case 41: crc32c_narrow_kernel<8, true, 256><<<grid, 256, 0, s>>>(a); break;
+      case 42: crc32c_narrow_kernel<16, true, 256, true><<<grid, 256, 0, s>>>(a); break;
 #endif
       case 9: crc32c_narrow_kernel<4, true, 512, true><<<grid, 512, 0, s>>>(a); break;
       case 20: crc32c_narrow_sorted_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
