@@ -300,6 +300,15 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     uint64_t r = 1;
     for (; r + 2 * kG <= K; r += kG) {  // full group in A, another full group after it: no next item yet
       uint4 B[kG];
+      if (kAbl == 5) {  // diag variant (exact): fold the group, then load the next one (no rows in flight meanwhile)
+#pragma unroll
+        for (int i = 0; i < kG; ++i) KVSEP_ROW(s.A[i]);
+        __builtin_amdgcn_sched_barrier(0);
+        KVSEP_LOADB(r + kG, false);
+#pragma unroll
+        for (int i = 0; i < kG; ++i) s.A[i] = B[i];
+        continue;
+      }
       KVSEP_LOADB(r + kG, false);  // rows r+kG .. r+2kG-1 <= K-1: no clamp
 #pragma unroll
       for (int i = 0; i < kG; ++i) KVSEP_ROW(s.A[i]);
@@ -1431,6 +1440,65 @@ __global__ void __launch_bounds__(512) stream_read_kernel(uintptr_t src, uint64_
   if (acc == 0x9e3779b9u) atomicXor(sink, acc);  // keeps the loads live; practically never stores
 }
 
+#ifdef KVSEP_DIAG
+// Diagnostic (wrong results by design): does a read pattern keep its rate once every row goes through the CRC
+// kernel's Z_1024 fold chain?  kWgChunk: the ceiling's pattern above (the workgroup's waves interleave the rows of
+// one 1 MiB chunk); else per-wave contiguous 128 KiB chunks, round-robin (the CRC kernel's piece pattern).  Each lane
+// folds its 16 B per row into 4 chains through the replicated LDS table, as crc32c_pieces_kernel does.
+template <bool kWgChunk, int kRows>
+__global__ void __launch_bounds__(512) stream_fold_kernel(uintptr_t src, uint64_t n16, uint32_t* sink,
+                                                          const DevTables* tabs) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  fill_lds<512>(lds, &tabs->z1024[0][0], tabs, threadIdx.x);
+  __syncthreads();
+  const uint32_t lc0 = (lane & 31u) << 2, lc1 = lc0 | 0x10000u;
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+  if (kWgChunk) {
+    constexpr uint64_t kChunk = 1u << 20;
+    constexpr uint64_t kStep = 8 * kRows * kRowBytes;
+    const uint64_t nchunks = n16 * 16 / kChunk;
+    for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+      const uintptr_t p = src + c * kChunk + uintptr_t(w) * kRowBytes + lane * 16u;
+#pragma unroll 1
+      for (uint64_t r = 0; r < kChunk; r += kStep) {
+        uint4 v[kRows];
+#pragma unroll
+        for (int u = 0; u < kRows; ++u) v[u] = ld16<true>(p + r + uint64_t(u) * 8 * kRowBytes);
+#pragma unroll
+        for (int u = 0; u < kRows; ++u) {
+          c0 = fold_step(lds, c0, v[u].x, lc0, lc1);
+          c1 = fold_step(lds, c1, v[u].y, lc0, lc1);
+          c2 = fold_step(lds, c2, v[u].z, lc0, lc1);
+          c3 = fold_step(lds, c3, v[u].w, lc0, lc1);
+        }
+      }
+    }
+  } else {
+    constexpr uint64_t kChunk = 128u << 10;
+    const uint64_t nchunks = n16 * 16 / kChunk, nwaves = uint64_t(gridDim.x) * 8;
+    for (uint64_t c = uint64_t(w) * gridDim.x + blockIdx.x; c < nchunks; c += nwaves) {
+      const uintptr_t p = src + c * kChunk + lane * 16u;
+#pragma unroll 1
+      for (uint64_t r = 0; r < kChunk; r += kRows * kRowBytes) {
+        uint4 v[kRows];
+#pragma unroll
+        for (int u = 0; u < kRows; ++u) v[u] = ld16<true>(p + r + uint64_t(u) * kRowBytes);
+#pragma unroll
+        for (int u = 0; u < kRows; ++u) {
+          c0 = fold_step(lds, c0, v[u].x, lc0, lc1);
+          c1 = fold_step(lds, c1, v[u].y, lc0, lc1);
+          c2 = fold_step(lds, c2, v[u].z, lc0, lc1);
+          c3 = fold_step(lds, c3, v[u].w, lc0, lc1);
+        }
+      }
+    }
+  }
+  const uint32_t acc = c0 ^ c1 ^ c2 ^ c3;
+  if (acc == 0x9e3779b9u) atomicXor(sink, acc);
+}
+#endif
+
 }  // namespace kvsep
 
 // ================================================================================================
@@ -1643,6 +1711,8 @@ void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs
   // LDS-lookup overlap; so was staging items two ahead, -1.5 % on the Zipf batch)
   //   5: 16-wave workgroups (the round-1 kernel)    6: 12-wave workgroups    7: 4-wave workgroups, 8-row groups
   //   10: rows ending at the 16-B aligned end (before the 128-B grid)
+  //   22 / 24: 2- / 3-row groups; 23 / 25: 4- / 8-row groups folded before the next group loads (exact; measured
+  //   slower or equal)
   //   8, 9, 11, 12: diagnostic ablations (wrong results): no lane merge, XOR folds, no head/tail steps, no tree
   // Only the default is compiled into the shipped library; the rest exist in the KVSEP_DIAG tools build
   // (`make -C kv-separate_amd diag` -> tools/libkvsep_diag.so).
@@ -1660,6 +1730,10 @@ void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs
     case 10: crc32c_pieces_kernel<P, D, 4, true, true, 0, T, false><<<grid, T, 0, s>>>(a); break;  // 16-B rows
     case 11: crc32c_pieces_kernel<P, D, 4, true, true, 3, T><<<grid, T, 0, s>>>(a); break;  // ablation: no head/tail
     case 12: crc32c_pieces_kernel<P, D, 4, true, true, 4, T><<<grid, T, 0, s>>>(a); break;  // ablation: no lane tree
+    case 22: crc32c_pieces_kernel<P, D, 2, true, true, 0, T><<<grid, T, 0, s>>>(a); break;  // 2-row groups
+    case 23: crc32c_pieces_kernel<P, D, 4, true, true, 5, T><<<grid, T, 0, s>>>(a); break;  // unpipelined groups
+    case 24: crc32c_pieces_kernel<P, D, 3, true, true, 0, T><<<grid, T, 0, s>>>(a); break;  // 3-row groups
+    case 25: crc32c_pieces_kernel<P, D, 8, true, true, 5, T><<<grid, T, 0, s>>>(a); break;  // unpipelined, 8 rows
     case 14:  // guided grabs of remaining / (d nwaves), d = 1, 2, 8, 16, 32, 4 (default: adaptive)
     case 15:
     case 17:
@@ -2099,6 +2173,15 @@ int kvsep_stream_read_device(kvsep_crc32c_ctx* c, void* stream, const void* src,
     e1 = take_event(c);
     if (e0 && e1) KVSEP_HIP(hipEventRecord(e0, s));
   }
+#ifdef KVSEP_DIAG  // KVSEP_CRC_VARIANT 31-34: the read patterns with the fold chain (stream_fold_kernel)
+  if (c->variant >= 31 && c->variant <= 34) {
+    const uintptr_t sp = reinterpret_cast<uintptr_t>(src);
+    if (c->variant == 31) stream_fold_kernel<true, 8><<<unsigned(c->num_cus), 512, 0, s>>>(sp, n16, sink, c->d_tabs);
+    if (c->variant == 32) stream_fold_kernel<true, 4><<<unsigned(c->num_cus), 512, 0, s>>>(sp, n16, sink, c->d_tabs);
+    if (c->variant == 33) stream_fold_kernel<false, 8><<<unsigned(c->num_cus), 512, 0, s>>>(sp, n16, sink, c->d_tabs);
+    if (c->variant == 34) stream_fold_kernel<false, 4><<<unsigned(c->num_cus), 512, 0, s>>>(sp, n16, sink, c->d_tabs);
+  } else
+#endif
   stream_read_kernel<<<unsigned(c->num_cus), 512, 0, s>>>(reinterpret_cast<uintptr_t>(src), n16, sink);
   KVSEP_HIP(hipGetLastError());
   if (c->timing && e0 && e1) {

@@ -72,8 +72,8 @@ def main():
         wide = code.endswith("w")  # "<variant>w": the wide kernel even where the narrow one would be chosen
         if wide:
             code = code[:-1]
-        if code.endswith("s") or code.endswith("d"):  # "<variant>s" / "<variant>d": static / guided schedule
-            sched, code = code[-1] == "d", code[:-1]
+        if code[-1:] in ("s", "d", "r"):  # "<variant>s" / "d" / "r": static contiguous / guided / static round-robin
+            sched, code = {"s": False, "d": True, "r": "rr"}[code[-1]], code[:-1]
         if "p" in code:  # "<variant>p<KiB>": that variant with its own piece size, e.g. 1p128 vs 1p1024
             code, pk = code.split("p")
             piece_kib = int(pk)
