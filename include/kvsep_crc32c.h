@@ -46,9 +46,15 @@ uint32_t kvsep_crc32c_unmask(uint32_t masked_crc);       /* util/crc32c.h:35-38 
 /* port/port_stdcxx.h:142: returns Extend(crc, buf, size); never 0 for the self-test buffer. */
 uint32_t kvsep_accelerated_crc32c(uint32_t crc, const char* buf, size_t size);
 void kvsep_set_offload_threshold(uint64_t nbytes);
+/* A call at/above the threshold while another caller holds the device's GPU leg: wait != 0 queues it for the
+ * GPU; wait == 0 (the default) runs it on the host leg at once -- the reference calls Extend from the writer,
+ * compaction, GC and reader threads concurrently (db/db_impl.cc:1829-1833), and one PCIe link serves one
+ * staged copy at a time while every core can run the host leg. */
+void kvsep_set_offload_wait(int wait);
 /* Counters of the scalar drop-in since load (any may be null): calls served by the GPU, calls served by
- * the host path below the threshold, and calls at/above the threshold that the GPU could not serve and
- * that finished on the host (set KVSEP_STRICT_GPU=1 to abort on those instead). */
+ * the host path (below the threshold, or diverted because the GPU leg was busy), and calls at/above the
+ * threshold that the GPU could not serve and that finished on the host (set KVSEP_STRICT_GPU=1 to abort on
+ * those instead). */
 void kvsep_offload_stats(uint64_t* gpu_calls, uint64_t* host_calls, uint64_t* gpu_failures);
 /* Host-only CRC (SSE4.2 crc32 instructions, 3-way interleaved): the small-input leg of Extend. */
 uint32_t kvsep_crc32c_extend_host(uint32_t init_crc, const char* data, size_t n);

@@ -343,7 +343,9 @@ int big_block(kvsep_crc32c_ctx* c, HostStaging& s, SlotJob* jobs, uint32_t* out,
 // The drop-in's context: one per device, on the CALLER's current device (a rank bound to GPU N checksums on
 // GPU N), created on first use.
 constexpr int kMaxDevices = 64;
-kvsep_crc32c_ctx* default_ctx() {
+std::atomic<bool> g_dropin_busy[kMaxDevices];  // a caller holds that device's drop-in GPU leg
+std::atomic<int> g_offload_wait{0};             // kvsep_set_offload_wait
+kvsep_crc32c_ctx* default_ctx(int* dev_out) {
   static std::once_flag once[kMaxDevices];
   static kvsep_crc32c_ctx* ctx[kMaxDevices] = {};
   int dev = 0;
@@ -352,6 +354,7 @@ kvsep_crc32c_ctx* default_ctx() {
     return nullptr;
   }
   if (dev < 0 || dev >= kMaxDevices) return nullptr;
+  *dev_out = dev;
   std::call_once(once[dev], [dev] {
     if (kvsep_crc32c_ctx_create(dev, &ctx[dev]) != KVSEP_OK) {
       std::fprintf(stderr, "kvsep_crc32c: GPU offload unavailable on device %d: %s\n", dev, kvsep_last_error());
@@ -392,11 +395,22 @@ uint32_t kvsep_crc32c_extend_host(uint32_t init_crc, const char* data, size_t n)
 
 uint32_t kvsep_crc32c_extend(uint32_t init_crc, const char* data, size_t n) {
   if (n >= g_offload_threshold.load(std::memory_order_relaxed)) {
-    kvsep_crc32c_ctx* c = default_ctx();
+    int dev = 0;
+    kvsep_crc32c_ctx* c = default_ctx(&dev);
     if (c) {
+      // busy GPU leg and no waiting: this caller takes the host leg now (exact either way) instead of queueing
+      // behind the staged copy of another caller on the same PCIe link
+      const bool wait = g_offload_wait.load(std::memory_order_relaxed) != 0;
+      bool idle = false;
+      if (!wait && !g_dropin_busy[dev].compare_exchange_strong(idle, true, std::memory_order_acquire)) {
+        g_host_calls.fetch_add(1, std::memory_order_relaxed);
+        return host_crc(init_crc, reinterpret_cast<const uint8_t*>(data), n);
+      }
       const uint64_t off = 0, len = n;
       uint32_t out = 0;
-      if (kvsep_crc32c_batch_host_span(c, data, n, &off, &len, &init_crc, &out, 1) == KVSEP_OK) {
+      const int rc = kvsep_crc32c_batch_host_span(c, data, n, &off, &len, &init_crc, &out, 1);
+      if (!wait) g_dropin_busy[dev].store(false, std::memory_order_release);
+      if (rc == KVSEP_OK) {
         g_gpu_calls.fetch_add(1, std::memory_order_relaxed);
         return out;
       }
@@ -425,6 +439,8 @@ uint32_t kvsep_accelerated_crc32c(uint32_t crc, const char* buf, size_t size) {
 }
 
 void kvsep_set_offload_threshold(uint64_t nbytes) { g_offload_threshold.store(nbytes); }
+
+void kvsep_set_offload_wait(int wait) { g_offload_wait.store(wait != 0 ? 1 : 0); }
 
 void kvsep_offload_stats(uint64_t* gpu_calls, uint64_t* host_calls, uint64_t* gpu_failures) {
   if (gpu_calls) *gpu_calls = g_gpu_calls.load();

@@ -50,6 +50,7 @@ _SIGS = {
     "kvsep_crc32c_unmask": (ctypes.c_uint32, [ctypes.c_uint32]),
     "kvsep_accelerated_crc32c": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
     "kvsep_set_offload_threshold": (None, [ctypes.c_uint64]),
+    "kvsep_set_offload_wait": (None, [ctypes.c_int]),
     "kvsep_offload_stats": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "kvsep_crc32c_kernel_name": (ctypes.c_char_p, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]),
     "kvsep_crc32c_extend_host": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),

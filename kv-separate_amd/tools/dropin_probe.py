@@ -46,8 +46,11 @@ def main():
         p = buf.ctypes.data
         want = kvsep.extend_host(0, buf)
         row = {"bytes": n}
-        for name, thr in (("host", 1 << 62), ("gpu", 0)):
+        # gpu: every call queues for the GPU leg (wait 1); divert: the default policy, a caller that finds the GPU
+        # leg busy runs the host leg (wait 0)
+        for name, thr, wait in (("host", 1 << 62, 1), ("gpu", 0, 1), ("divert", 0, 0)):
             L.kvsep_set_offload_threshold(thr)
+            L.kvsep_set_offload_wait(wait)
             assert L.kvsep_crc32c_extend(0, p, n) == want
             for threads in (1, 8):
                 g, us = rate(lambda: L.kvsep_crc32c_extend(0, p, n), n, threads)
@@ -56,6 +59,7 @@ def main():
         print(json.dumps(row), flush=True)
         rows.append(row)
     L.kvsep_set_offload_threshold(64 << 20)
+    L.kvsep_set_offload_wait(0)
     if len(sys.argv) > 1:
         with open(sys.argv[1], "w") as f:
             json.dump(rows, f, indent=1)

@@ -408,7 +408,10 @@ int main(int argc, char** argv) {
   const std::string dir = argc > 1 ? argv[1] : "";
   const bool gpu = argc > 2 && std::strcmp(argv[2], "gpu") == 0;
 #ifdef KVSEP_CALLSITE
-  if (gpu) kvsep_set_offload_threshold(0);  // every Extend of the reference call sites on the GPU
+  if (gpu) {  // every Extend of the reference call sites on the GPU
+    kvsep_set_offload_threshold(0);
+    kvsep_set_offload_wait(1);
+  }
 #else
   if (gpu) {
     std::fprintf(stderr, "gpu mode needs the KVSEP_CALLSITE build\n");

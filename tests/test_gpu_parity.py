@@ -270,6 +270,7 @@ def offload_stats():
 
 def test_dropin_extend_offload_path(golden):
     kvsep.lib().kvsep_set_offload_threshold(1)  # force every non-empty Extend through the GPU
+    kvsep.lib().kvsep_set_offload_wait(1)
     gpu0, host0, fail0 = offload_stats()
     try:
         calls = 0
@@ -282,6 +283,7 @@ def test_dropin_extend_offload_path(golden):
         calls += 4
     finally:
         kvsep.lib().kvsep_set_offload_threshold(64 << 20)
+        kvsep.lib().kvsep_set_offload_wait(0)
     gpu1, host1, fail1 = offload_stats()
     # every one of those calls ran on the GPU: none on the host leg, no silent host fallback
     assert (gpu1 - gpu0, fail1 - fail0) == (calls, 0)
@@ -295,6 +297,7 @@ def test_dropin_extend_concurrent_threads(oracle):
     exp = [oracle.extend(0, b) for b in bufs]
     got = [None] * 8
     kvsep.lib().kvsep_set_offload_threshold(1)
+    kvsep.lib().kvsep_set_offload_wait(1)  # queue for the GPU leg: every call on the GPU
     gpu0, _, fail0 = offload_stats()
     try:
         def work(i):
@@ -306,9 +309,36 @@ def test_dropin_extend_concurrent_threads(oracle):
             t.join()
     finally:
         kvsep.lib().kvsep_set_offload_threshold(64 << 20)
+        kvsep.lib().kvsep_set_offload_wait(0)
     gpu1, _, fail1 = offload_stats()
     assert got == [[e] * 5 for e in exp]
     assert (gpu1 - gpu0, fail1 - fail0) == (40, 0)
+
+
+def test_dropin_extend_busy_diverts_to_host(oracle):
+    """Default policy (kvsep_set_offload_wait(0)): a caller that finds the device's GPU leg busy runs the host leg
+    at once instead of queueing.  8 threads over the threshold: every result bit-exact, every call counted on the
+    GPU or the host leg, none a GPU failure."""
+    import threading
+    bufs = [splitmix64_bytes((2 << 20) + 4099 * i, 90 + i, 0).tobytes() for i in range(8)]
+    exp = [oracle.extend(0, b) for b in bufs]
+    got = [None] * 8
+    kvsep.lib().kvsep_set_offload_threshold(1)
+    gpu0, host0, fail0 = offload_stats()
+    try:
+        def work(i):
+            got[i] = [kvsep.value(bufs[i]) for _ in range(5)]
+        ts = [threading.Thread(target=work, args=(i,)) for i in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    finally:
+        kvsep.lib().kvsep_set_offload_threshold(64 << 20)
+    gpu1, host1, fail1 = offload_stats()
+    assert got == [[e] * 5 for e in exp]
+    assert (gpu1 - gpu0) + (host1 - host0) == 40 and fail1 == fail0
+    assert gpu1 > gpu0  # the idle leg was taken at least once
 
 
 def test_split_invariance_full_cfg3_scale(ctx):
