@@ -68,9 +68,6 @@ struct PiecesArgs {
   const uint64_t* len;
   const uint32_t* init;             // nullable -> 0
   uint32_t* out;
-  const uint32_t* expect;           // nullable: verify mode
-  unsigned long long* first_bad;
-  unsigned long long* nbad;
   uint64_t count;
   const uint64_t* pstart;           // planned mode: piece range of block b = [pstart[b], pstart[b+1]) (u64: an
                                     // understated total_bytes cannot wrap the scan, see the max_pieces fallback)
@@ -420,13 +417,8 @@ __device__ uint32_t gf2_shift(const DevTables* tabs, uint32_t reg, uint64_t n) {
   return gf2_mulmod(p, reg);
 }
 
-__device__ __forceinline__ void emit_block(const PiecesArgs& a, uint64_t b, uint32_t crc) {
-  a.out[b] = crc;
-  if (a.expect && mask_crc(crc) != a.expect[b]) {
-    atomicMin(a.first_bad, (unsigned long long)b);
-    atomicAdd(a.nbad, 1ull);
-  }
-}
+// The CRC kernels only store the result; the verify form's Mask/compare runs after them (verify_finish_kernel).
+__device__ __forceinline__ void emit_block(const PiecesArgs& a, uint64_t b, uint32_t crc) { a.out[b] = crc; }
 
 // LDS image of a CRC workgroup: the replicated fold table `rep` (4 byte-tables) at [0, 128 KiB), then the
 // small tables (Z_4, the tree tables, the byte table) as one contiguous run.
@@ -1196,7 +1188,7 @@ __device__ __forceinline__ void wave_sort64(uint32_t& key, uint32_t& idx, uint32
 // slot s takes the block at sorted position 8k + s (two ds_bpermutes to find it, four to fetch its descriptor).
 // The rows, the slot tree and the end path are the narrow kernel's (nstage / nfinish); blocks over the hint go to
 // narrow_deferred as there.
-template <int kG, bool kNT, int kThreads>
+template <int kG, bool kNT, int kThreads, bool kDrain = false>  // kDrain: diag, vmcnt(0) after each group's emit
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   constexpr uint32_t kPerGroup = 64 / kNarrowLanes;
@@ -1308,6 +1300,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesAr
         }
       });
       if (j == kNarrowLanes - 1 && ia.live) emit_block(a, ia.w + ia.src, ~reg);
+      if (kDrain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (here) {
         ++k;
         return true;
@@ -1355,6 +1348,25 @@ __global__ void crc32c_plan_count_kernel(const uint64_t* len, uint64_t count, ui
   // up with a short remainder piece that costs a work item of its own (3b: 33-B pieces, one per record);
   // only the later pieces must be exactly P long for the combine's Z_P.
   counts[b] = n < 2 * piece_bytes ? 1u : n / piece_bytes;
+}
+
+// Verify form: the Mask/compare of db/value_log_reader.cc:109-122 (and table/format.cc:102-106) as one pass over
+// the u32 results after the CRC kernels, never inside them.  Inside a kernel's pipeline the compare's load of
+// expect[b] drained every staged load of the next item (vmcnt(0)) at each block, and with the compare there the
+// sorted-window kernel returned wrong CRCs from the third group of a window on (found by tools/soak.py; DESIGN
+// §3.2).  Wave-level reduction: one atomicMin / atomicAdd per wave that saw a mismatch.
+__global__ void __launch_bounds__(256) verify_finish_kernel(const uint32_t* out, const uint32_t* expect,
+                                                            uint64_t count, unsigned long long* first_bad,
+                                                            unsigned long long* nbad) {
+  const uint64_t b = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const bool bad = b < count && mask_crc(out[b]) != expect[b];
+  const uint64_t m = __builtin_amdgcn_ballot_w64(bad);
+  if (!m) return;
+  const uint32_t lane = threadIdx.x & 63u;
+  if (lane == uint32_t(__builtin_ctzll(m))) {  // the wave's first bad block is its lowest bad index
+    atomicMin(first_bad, (unsigned long long)b);
+    atomicAdd(nbad, (unsigned long long)__builtin_popcountll(m));
+  }
 }
 
 // SST write side (table/table_builder.cc:222-225): crc = Extend(Value(block), &type, 1); trailer word = Mask(crc).
@@ -1800,7 +1812,6 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
   a.len = len;
   a.init = init;
   a.out = out;
-  a.expect = expect;
   a.count = count;
   a.piece_bytes = planned ? piece_for(c, total_bytes, &a.zpiece) : c->piece_bytes;
   a.tabs = c->d_tabs;
@@ -1810,8 +1821,6 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
       first_bad = reinterpret_cast<uint64_t*>(sc.d_verify);
       nbad = reinterpret_cast<uint64_t*>(sc.d_verify + 1);
     }
-    a.first_bad = reinterpret_cast<unsigned long long*>(first_bad);
-    a.nbad = reinterpret_cast<unsigned long long*>(nbad);
     KVSEP_HIP(hipMemsetAsync(first_bad, 0xff, 8, s));
     KVSEP_HIP(hipMemsetAsync(nbad, 0, 8, s));
   }
@@ -1878,6 +1887,7 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
       case 17: crc32c_narrow_kernel<4, true, 512, true, 1><<<grid, 512, 0, s>>>(a); break;    // ablation
       case 21: crc32c_narrow_sorted_kernel<4, true, 512><<<grid, 512, 0, s>>>(a); break;
       case 22: crc32c_narrow_sorted_kernel<4, true, 768><<<grid, 768, 0, s>>>(a); break;
+      case 23: crc32c_narrow_sorted_kernel<4, true, 1024, true><<<grid, 1024, 0, s>>>(a); break;  // drain per group
       // compact 80 KiB LDS image (two workgroups per CU): 30 / 34: 8-wave workgroups, two per CU, persistent (34:
       // fill overlapped); 31 / 35: one 8-block group per wave, grid over the whole batch (the dispatcher balances);
       // 32: two groups per wave; 33: 16-wave workgroups, one per CU (the conflict cost alone)
@@ -1920,6 +1930,11 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
   }
   if (planned) {
     crc32c_combine_kernel<<<unsigned((count + 255) / 256), 256, 0, s>>>(a);
+    KVSEP_HIP(hipGetLastError());
+  }
+  if (expect) {
+    verify_finish_kernel<<<unsigned((count + 255) / 256), 256, 0, s>>>(
+        out, expect, count, reinterpret_cast<unsigned long long*>(first_bad), reinterpret_cast<unsigned long long*>(nbad));
     KVSEP_HIP(hipGetLastError());
   }
   return KVSEP_OK;

@@ -152,6 +152,37 @@ def test_sorted_windows_ragged(oracle, pool, count):
 
 
 @pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted"])
+@pytest.mark.parametrize("count", [70000, 200000])
+def test_verify_several_groups_per_wave(oracle, pool, kernel, count):
+    """Verify form with several 8-block groups per wave (3 and 7 per 64-block window at these counts): the sorted
+    kernel once returned wrong CRCs from the third group of a window on in this form only (tools/soak.py); the
+    compare now runs after the kernel (verify_finish_kernel).  Random offsets (overlapping), ragged short lengths,
+    planted mismatches."""
+    data, d = pool
+    rng = np.random.default_rng(count)
+    ln = rng.integers(0, 201, count).astype(np.uint64)
+    off = rng.integers(0, data.size - 256, count).astype(np.uint64)
+    exp = oracle.batch(data, off, ln, threads=8)
+    masked = np.array([oracle.lib.oracle_crc32c_mask(int(c)) for c in exp], np.uint32)
+    bad = sorted({5, count // 3, count - 2})
+    masked[bad] ^= 0x100
+    ctx = kvsep.Context(0)
+    try:
+        ctx.set_kernel(kernel)
+        out = torch.zeros(count, dtype=torch.int32, device=DEV)
+        fb = torch.zeros(1, dtype=torch.int64, device=DEV)
+        nb = torch.zeros(1, dtype=torch.int64, device=DEV)
+        ctx.verify_device(d.data_ptr(), dev_u64(off), dev_u64(ln), dev_u32(masked), out, fb, nb,
+                          total_bytes=int(ln.sum()), max_len=int(ln.max()))
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), exp)
+        assert (fb.item(), nb.item()) == (bad[0], len(bad))
+        assert np.array_equal(run(ctx, d, off, ln), exp)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted"])
 def test_every_end_geometry(oracle, pool, kernel):
     """Every case of the slot's end path: m = 0..7 whole 16-B chunks between the 128-B grid and the 16-B end (m = 7
     uses all of lanes 0..6 of the tail load), each with head and tail bytes 0..15, with and without body rows."""
