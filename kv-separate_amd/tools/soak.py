@@ -2,8 +2,9 @@
 """Randomised bit-exactness soak of the shipped library against the oracle, time-bounded: batch shapes the test
 suite samples only sparsely -- up to 200 K blocks, length mixes (uniform, Zipf, around 4 KiB, tiny, mixed with
 long), any byte offset, overlapping blocks, random or no inits -- through every kernel choice (auto, wide, narrow16,
-narrow8, sorted), every hint kind (none, exact, loose, understated), three piece sizes, and the verify form with
-corrupted expectations.  Every result is compared with the oracle on the same bytes; prints one line per case and
+narrow8, sorted), every hint kind (none, exact, loose, understated), three piece sizes, the verify form with
+corrupted expectations, and the host forms (pinned-staged span, pointer per block, a two-member device group) and
+a hipGraph-captured device call.  Every result is compared with the oracle on the same bytes; prints one line per case and
 a summary, exits non-zero on the first mismatch.  usage: soak.py [--seconds 240] [--seed N]"""
 import argparse
 import os
@@ -61,6 +62,7 @@ def main():
                 c.set_piece_bytes(piece)
             c.set_kernel(k)
             ctxs[(piece, k)] = c
+    group = kvsep.Group([0, 0])  # two contexts on the one GPU: the byte-balanced split and the merged results
     u64 = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64)).to(dev)  # noqa: E731
     t_end = time.time() + args.seconds
     cases = blocks = nbytes = 0
@@ -89,7 +91,40 @@ def main():
         exp = oracle.batch(host, off, ln, init, threads=8)
         d_init = torch.from_numpy(init.view(np.int32)).to(dev) if init is not None else None
         out = torch.zeros(n, dtype=torch.int32, device=dev)
-        verify = rng.random() < 0.3
+        form = str(rng.choice(["device", "device", "device", "host_span", "host_ptrs", "group", "graph"]))
+        verify = form == "device" and rng.random() < 0.4
+        if form != "device":
+            if form == "host_span":
+                got = ctx.batch_host_span(host, off, ln, init)
+            elif form == "host_ptrs":
+                k = min(n, 4096)  # one Python buffer object per block
+                sub = [memoryview(host)[int(off[i]):int(off[i] + ln[i])] for i in range(k)]
+                got = np.concatenate([ctx.batch_host(sub, None if init is None else init[:k]),
+                                      np.asarray(exp[k:], np.uint32)])
+            elif form == "group":
+                got = group.batch_host_span(host, off, ln, init)
+            else:  # graph: capture one device call, replay it twice
+                ctx.reserve(n, int(ln.sum()))
+                out = torch.zeros(n, dtype=torch.int32, device=dev)
+                d_off, d_len = u64(off), u64(ln)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    ctx.batch_device(d.data_ptr(), d_off, d_len, out, init=d_init, max_len=max_len,
+                                     total_bytes=int(ln.sum()), stream=torch.cuda.current_stream())
+                out.zero_()
+                g.replay()
+                g.replay()
+                torch.cuda.synchronize()
+                got = out.cpu().numpy().view(np.uint32)
+            mism = int(np.count_nonzero(np.asarray(got, np.uint32) != exp))
+            cases += 1
+            blocks += n
+            nbytes += int(ln.sum())
+            print(f"case {cases}: n={n} {kind} hint={hint}({max_len}) piece={piece} kernel={kern} form={form} -> "
+                  f"{'ok' if not mism else f'{mism} MISMATCHES'}", flush=True)
+            if mism:
+                sys.exit(1)
+            continue
         if verify:
             masked = np.array([kvsep.mask(int(x)) for x in exp], dtype=np.uint32)
             bad = rng.random(n) < 0.01
