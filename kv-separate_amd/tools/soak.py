@@ -5,7 +5,8 @@ long), any byte offset, overlapping blocks, random or no inits -- through every 
 narrow8, sorted), every hint kind (none, exact, loose, understated), three piece sizes, the verify form with
 corrupted expectations, and the host forms (pinned-staged span, pointer per block, a two-member device group) and
 a hipGraph-captured device call.  Every result is compared with the oracle on the same bytes; prints one line per case and
-a summary, exits non-zero on the first mismatch.  usage: soak.py [--seconds 240] [--seed N]"""
+a summary, exits non-zero on the first mismatch.  usage: soak.py [--seconds 240] [--seed N]
+tests/test_gpu_soak.py runs a fixed, seeded number of these cases (soak(seed, max_cases=...)) in the -m gpu suite."""
 import argparse
 import os
 import sys
@@ -43,16 +44,18 @@ def lengths(rng, n, kind):
     return ln
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--seconds", type=float, default=240)
-    ap.add_argument("--seed", type=int, default=int(time.time()) & 0xFFFFFFFF)
-    args = ap.parse_args()
-    print(f"seed {args.seed}", flush=True)
-    rng = np.random.default_rng(args.seed)
+class Mismatch(AssertionError):
+    pass
+
+
+def soak(seed, seconds=None, max_cases=None, log=print, pool=POOL):
+    """Random cases until `seconds` elapse or `max_cases` ran; raises Mismatch on the first wrong result.
+    -> (cases, blocks, bytes)."""
+    POOL = pool  # noqa: N806
+    rng = np.random.default_rng(seed)
     oracle = load_oracle()
     dev = torch.device("cuda:0")
-    host = splitmix64_bytes(POOL, args.seed, 0)
+    host = splitmix64_bytes(POOL, seed, 0)
     d = torch.from_numpy(host).to(dev)
     ctxs = {}
     for piece in (None, 4096, 64 * 1024):
@@ -64,9 +67,9 @@ def main():
             ctxs[(piece, k)] = c
     group = kvsep.Group([0, 0])  # two contexts on the one GPU: the byte-balanced split and the merged results
     u64 = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64)).to(dev)  # noqa: E731
-    t_end = time.time() + args.seconds
+    t_end = time.time() + seconds if seconds else float("inf")
     cases = blocks = nbytes = 0
-    while time.time() < t_end:
+    while time.time() < t_end and (max_cases is None or cases < max_cases):
         n = int(rng.choice([1, 7, 64, 513, 4096, 20000, 70000, 200000]))
         kind = str(rng.choice(["uniform", "zipf", "sst", "tiny", "mixed"]))
         ln = np.clip(lengths(rng, n, kind), 0, POOL // 4).astype(np.uint64)
@@ -120,10 +123,11 @@ def main():
             cases += 1
             blocks += n
             nbytes += int(ln.sum())
-            print(f"case {cases}: n={n} {kind} hint={hint}({max_len}) piece={piece} kernel={kern} form={form} -> "
-                  f"{'ok' if not mism else f'{mism} MISMATCHES'}", flush=True)
+            msg = (f"case {cases}: n={n} {kind} hint={hint}({max_len}) piece={piece} kernel={kern} form={form} -> "
+                   f"{'ok' if not mism else f'{mism} MISMATCHES'}")
+            log(msg)
             if mism:
-                sys.exit(1)
+                raise Mismatch(f"seed {seed}: {msg}")
             continue
         if verify:
             masked = np.array([kvsep.mask(int(x)) for x in exp], dtype=np.uint32)
@@ -147,11 +151,28 @@ def main():
         cases += 1
         blocks += n
         nbytes += int(ln.sum())
-        print(f"case {cases}: n={n} {kind} hint={hint}({max_len}) piece={piece} kernel={kern} "
-              f"({ctx.kernel_name(n, max_len, int(ln.sum()))}) verify={verify} -> {'ok' if ok else f'{mism} MISMATCHES'}",
-              flush=True)
+        msg = (f"case {cases}: n={n} {kind} hint={hint}({max_len}) piece={piece} kernel={kern} "
+               f"({ctx.kernel_name(n, max_len, int(ln.sum()))}) verify={verify} -> {'ok' if ok else f'{mism} MISMATCHES'}")
+        log(msg)
         if not ok:
-            sys.exit(1)
+            raise Mismatch(f"seed {seed}: {msg}")
+    for c in ctxs.values():
+        c.close()
+    group.close()
+    return cases, blocks, nbytes
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=240)
+    ap.add_argument("--seed", type=int, default=int(time.time()) & 0xFFFFFFFF)
+    args = ap.parse_args()
+    print(f"seed {args.seed}", flush=True)
+    try:
+        cases, blocks, nbytes = soak(args.seed, seconds=args.seconds, log=lambda m: print(m, flush=True))
+    except Mismatch as e:
+        print(e, flush=True)
+        sys.exit(1)
     print(f"soak ok: {cases} cases, {blocks} blocks, {nbytes / 2**30:.2f} GiB, seed {args.seed}", flush=True)
 
 
