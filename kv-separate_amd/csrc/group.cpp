@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -22,6 +23,8 @@ struct kvsep_crc32c_group {
   std::vector<int> devices;
   std::vector<kvsep_crc32c_ctx*> ctx;
   std::vector<hipStream_t> stream;  // device-resident form: one stream per member, on its device
+  std::vector<uint64_t*> d_res;      // verify form: [first_bad, nbad] of each member's shard, on its device
+  std::mutex mu;                     // device-resident calls share the streams and d_res: one at a time
 };
 
 namespace {
@@ -85,14 +88,22 @@ int kvsep_crc32c_group_create(const int* devices, int ndev, kvsep_crc32c_group**
     kvsep_crc32c_ctx* c = nullptr;
     int rc = kvsep_crc32c_ctx_create(devices[i], &c);
     hipStream_t s = nullptr;
+    uint64_t* res = nullptr;
     if (rc == KVSEP_OK) {
       kvsep::DeviceGuard dg(devices[i]);
       if (dg.err != hipSuccess || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
         kvsep::set_last_error("group_create: stream creation failed");
         rc = KVSEP_EHIP;
+      } else if (hipMalloc(&res, 16) != hipSuccess) {  // once here: a hipFree per call would synchronise the device
+        kvsep::set_last_error("group_create: hipMalloc failed");
+        rc = KVSEP_ENOMEM;
       }
     }
     if (rc != KVSEP_OK) {
+      if (s) {
+        kvsep::DeviceGuard dg(devices[i]);
+        (void)hipStreamDestroy(s);
+      }
       if (c) kvsep_crc32c_ctx_destroy(c);
       kvsep_crc32c_group_destroy(g);
       return rc;
@@ -100,6 +111,7 @@ int kvsep_crc32c_group_create(const int* devices, int ndev, kvsep_crc32c_group**
     g->devices.push_back(devices[i]);
     g->ctx.push_back(c);
     g->stream.push_back(s);
+    g->d_res.push_back(res);
   }
   *out = g;
   return KVSEP_OK;
@@ -112,6 +124,7 @@ void kvsep_crc32c_group_destroy(kvsep_crc32c_group* g) {
       kvsep::DeviceGuard dg(g->devices[i]);
       (void)hipStreamSynchronize(g->stream[i]);
       (void)hipStreamDestroy(g->stream[i]);
+      (void)hipFree(g->d_res[i]);
     }
     kvsep_crc32c_ctx_destroy(g->ctx[i]);
   }
@@ -204,6 +217,7 @@ int kvsep_crc32c_group_verify_device(kvsep_crc32c_group* g, const void* const* b
     kvsep::set_last_error("group_batch_device: bad argument");
     return KVSEP_EINVAL;
   }
+  std::lock_guard<std::mutex> lk(g->mu);
   const int n = int(g->ctx.size());
   std::vector<uint64_t> fb(n, UINT64_MAX), nb(n, 0);
   const int rc = fan_out(n, [&](int i) {
@@ -214,12 +228,8 @@ int kvsep_crc32c_group_verify_device(kvsep_crc32c_group* g, const void* const* b
       return int(KVSEP_EHIP);
     }
     int r;
-    uint64_t* d_res = nullptr;  // [first_bad, nbad] of this shard
+    uint64_t* d_res = expected_masked ? g->d_res[i] : nullptr;  // [first_bad, nbad] of this shard
     if (expected_masked) {
-      if (hipMalloc(&d_res, 16) != hipSuccess) {
-        kvsep::set_last_error("hipMalloc failed");
-        return int(KVSEP_ENOMEM);
-      }
       r = kvsep_crc32c_verify_device(g->ctx[i], g->stream[i], base[i], off[i], len[i], init ? init[i] : nullptr,
                                      expected_masked[i], out[i], d_res, d_res + 1, count[i], total_bytes[i], max_len[i]);
     } else {
@@ -232,7 +242,8 @@ int kvsep_crc32c_group_verify_device(kvsep_crc32c_group* g, const void* const* b
     }
     if (r == KVSEP_OK && d_res) {
       uint64_t h[2];
-      if (hipMemcpy(h, d_res, 16, hipMemcpyDeviceToHost) != hipSuccess) {
+      if (hipMemcpyAsync(h, d_res, 16, hipMemcpyDeviceToHost, g->stream[i]) != hipSuccess ||
+          hipStreamSynchronize(g->stream[i]) != hipSuccess) {
         kvsep::set_last_error("hipMemcpy failed");
         r = KVSEP_EHIP;
       } else {
@@ -240,7 +251,6 @@ int kvsep_crc32c_group_verify_device(kvsep_crc32c_group* g, const void* const* b
         nb[i] = h[1];
       }
     }
-    if (d_res) (void)hipFree(d_res);
     return r;
   });
   if (rc) return rc;
