@@ -267,6 +267,51 @@ def check_results(plan_all, results, oracle):
     return {"blocks_checked_vs_reference": checked, "blocks_sampled_vs_oracle": sampled, "mismatches": mism}
 
 
+def live_pmc_traffic(args, timeout_s=240):
+    """HBM bytes per launch of the CRC kernel, measured on THIS box in this run: one separate
+    `rocprofv3 --pmc FETCH_SIZE --kernel-trace` pass (counters in their own run, MI355X_MICROARCH.md HBM section) of
+    the same config, as a child process after the timed region and after this process freed its batch; gfx950
+    FETCH_SIZE counts half the bytes of a wide coalesced stream, so bytes = FETCH_SIZE (KB) x 1024 x 2, averaged over
+    the CRC kernel's dispatches of the pass.  -> (bytes per launch, dispatches, None) or (None, 0, reason)."""
+    import csv
+    import shutil
+    import statistics
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(exe):
+        return None, 0, "rocprofv3 not found"
+    d = tempfile.mkdtemp(prefix="kvsep_pmc_", dir="/tmp")
+    cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--pmc", "FETCH_SIZE", "--kernel-trace", "-d", d, "-o", "pmc",
+           "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--config", args.config,
+           "--steps", "3", "--warmup", "1", "--no-cpu", "--roundtrip-gib", "0", "--pmc-live", "off", "--launch", "eager",
+           "--schedule", args.schedule] + (["--piece-kib", str(args.piece_kib)] if args.piece_kib else []) + \
+          (["--no-plan-hint"] if args.no_plan_hint else [])
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                        "ROLE_RANK", "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    env["TMPDIR"] = "/tmp"
+    try:
+        r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                           timeout=timeout_s + 30)
+        if r.returncode:
+            tail = r.stderr.decode(errors="replace").strip().splitlines()[-1:] or [""]
+            return None, 0, f"rocprofv3 pass exited {r.returncode}: {tail[0][:200]}"
+        vals = {}
+        with open(os.path.join(d, "pmc_counter_collection.csv")) as fh:
+            for row in csv.DictReader(fh):
+                if row["Counter_Name"] == "FETCH_SIZE" and ("crc32c_pieces_kernel" in row["Kernel_Name"] or
+                                                            "crc32c_narrow" in row["Kernel_Name"]):
+                    vals[row["Dispatch_Id"]] = vals.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
+        if not vals:
+            return None, 0, "no CRC kernel dispatch in the pass"
+        return int(statistics.mean(vals.values()) * 1024 * 2), len(vals), None
+    except Exception as e:  # the headline line never depends on the profiler
+        return None, 0, f"rocprofv3 pass failed: {e}"
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -277,6 +322,9 @@ def main():
     ap.add_argument("--piece-kib", type=int, default=0, help="work-item size (0 = library default)")
     ap.add_argument("--schedule", default="default", choices=["default", "static", "dynamic"])
     ap.add_argument("--no-plan-hint", action="store_true", help="pass max_len = 0 (force the planning pass)")
+    ap.add_argument("--pmc-live", default="auto", choices=["auto", "on", "off"],
+                    help="roofline.traffic from a rocprofv3 --pmc FETCH_SIZE pass of this config run here after the "
+                         "timed region (auto: at N = 1); else from the committed profiles/pmc_cfg<config>.json")
     ap.add_argument("--launch", default="graph", choices=["graph", "eager"],
                     help="timed steps as hipGraph replays (default; eager launches if capture fails) or eager")
     ap.add_argument("--graph-steps", type=int, default=0,
@@ -516,6 +564,7 @@ def main():
 
     traffic = None
     traffic_src = None
+    traffic_profile = None
     pmc_cfg = "3b" if args.config == "5" else args.config  # config 5's launches are config-3b launches
     if args.pmc_json is None:
         args.pmc_json = os.path.join(ROOT, "profiles", f"pmc_cfg{pmc_cfg}.json")
@@ -523,10 +572,22 @@ def main():
         try:
             pm = json.load(open(args.pmc_json))
             if pm.get("config") == pmc_cfg:
-                traffic = pm.get("hbm_bytes_per_launch")
+                traffic = traffic_profile = pm.get("hbm_bytes_per_launch")
                 traffic_src = os.path.relpath(args.pmc_json, ROOT) + " (rocprofv3 --pmc passes of the same config)"
         except Exception:
             traffic = None
+    if rank == 0 and (args.pmc_live == "on" or (args.pmc_live == "auto" and world == 1)):
+        # the child allocates its own batch: free this one first (config 4 is 150 GiB of the 288)
+        data = d_off = d_len = out = None  # noqa: F841
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        live, nl, why = live_pmc_traffic(args)
+        if live is not None:
+            traffic = live
+            traffic_src = (f"live: rocprofv3 --pmc FETCH_SIZE --kernel-trace pass of this config on this box after the "
+                           f"timed region (child process, {nl} CRC dispatches), FETCH_SIZE x 1024 x 2")
+        else:
+            log(f"[rank 0] live PMC pass unavailable ({why}); traffic from the committed profile")
 
     if rank == 0:
         line = {
@@ -549,7 +610,8 @@ def main():
                        "parallelism": f"shard{world} (independent blocks per GPU, no data-path collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved_gbps / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "traffic_source": traffic_src,
+                         "traffic_source": traffic_src, "traffic_committed_profile": traffic_profile,
+                         "traffic_over_algorithmic": traffic and round(traffic / useful, 4),
                          "kernel": kernel_name, "kernel_avg_ms": round(kern_avg_ms, 4), "kernel_timing": timing_note,
                          "algorithmic_bytes_per_launch": useful},
             "cpu_baseline": cpu,
