@@ -324,7 +324,8 @@ def main():
     ap.add_argument("--no-plan-hint", action="store_true", help="pass max_len = 0 (force the planning pass)")
     ap.add_argument("--pmc-live", default="auto", choices=["auto", "on", "off"],
                     help="roofline.traffic from a rocprofv3 --pmc FETCH_SIZE pass of this config run here after the "
-                         "timed region (auto: at N = 1); else from the committed profiles/pmc_cfg<config>.json")
+                         "timed region (auto: at N = 1 when not itself under rocprofv3); else from the committed "
+                         "profiles/pmc_cfg<config>.json")
     ap.add_argument("--launch", default="graph", choices=["graph", "eager"],
                     help="timed steps as hipGraph replays (default; eager launches if capture fails) or eager")
     ap.add_argument("--graph-steps", type=int, default=0,
@@ -576,7 +577,10 @@ def main():
                 traffic_src = os.path.relpath(args.pmc_json, ROOT) + " (rocprofv3 --pmc passes of the same config)"
         except Exception:
             traffic = None
-    if rank == 0 and (args.pmc_live == "on" or (args.pmc_live == "auto" and world == 1)):
+    # auto: at N = 1, and never when this process itself runs under a profiler (rocprofv3 exports ROCPROF_* to the
+    # program it profiles; a nested profiler pass would fight it for the counters)
+    under_profiler = any(k.startswith("ROCPROF") for k in os.environ)
+    if rank == 0 and (args.pmc_live == "on" or (args.pmc_live == "auto" and world == 1 and not under_profiler)):
         # the child allocates its own batch: free this one first (config 4 is 150 GiB of the 288)
         data = d_off = d_len = out = None  # noqa: F841
         torch.cuda.synchronize()

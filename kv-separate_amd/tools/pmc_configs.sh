@@ -7,7 +7,7 @@ O=$R/gpurun_out
 mkdir -p $O
 export TMPDIR=/tmp
 cd /tmp
-B="$R/bench.py --steps 3 --warmup 1 --no-cpu --roundtrip-gib 0"
+B="$R/bench.py --pmc-live off --steps 3 --warmup 1 --no-cpu --roundtrip-gib 0"
 for c in "$@"; do
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch_$c -o pmc --output-format csv -- python3 $B --config $c > $O/pmc_fetch_$c.log 2>&1 || exit 1
   timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum --kernel-trace -d $O/pmc_rdreq_$c -o pmc --output-format csv -- python3 $B --config $c > $O/pmc_rdreq_$c.log 2>&1 || exit 1

@@ -13,9 +13,9 @@ done
 timeout -k 10 300 python -u kv-separate_amd/tools/launch_floor_probe.py 64 256 1024 4096 > $O/launch_floor.txt 2>&1 || exit 1
 export TMPDIR=/tmp
 cd /tmp
-B="$R/bench.py --steps 3 --warmup 1 --no-cpu --roundtrip-gib 0"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o stats --output-format csv -- python3 $R/bench.py --steps 20 --warmup 1 --no-cpu --roundtrip-gib 0 --launch eager > $O/prof.json 2> $O/prof.err || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof2 -o stats --output-format csv -- python3 $R/bench.py --config 2 --steps 20 --warmup 1 --no-cpu --roundtrip-gib 0 > $O/prof2.json 2> $O/prof2.err || exit 1
+B="$R/bench.py --steps 3 --warmup 1 --no-cpu --roundtrip-gib 0 --pmc-live off"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o stats --output-format csv -- python3 $R/bench.py --steps 20 --warmup 1 --no-cpu --roundtrip-gib 0 --launch eager --pmc-live off > $O/prof.json 2> $O/prof.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof2 -o stats --output-format csv -- python3 $R/bench.py --config 2 --steps 20 --warmup 1 --no-cpu --roundtrip-gib 0 --pmc-live off > $O/prof2.json 2> $O/prof2.err || exit 1
 for c in 3a 3b 4 2; do
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch_$c -o pmc --output-format csv -- python3 $B --config $c > $O/pmc_fetch_$c.log 2>&1 || exit 1
   timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum --kernel-trace -d $O/pmc_rdreq_$c -o pmc --output-format csv -- python3 $B --config $c > $O/pmc_rdreq_$c.log 2>&1 || exit 1
