@@ -82,6 +82,11 @@ struct PiecesArgs {
                                     // 0: adaptive, clamp(total / (64 * nwaves), 4, 32)
   uint32_t guided_cap;              // dynamic schedule: at most this many items per grab (0: no cap)
   uint64_t hint;                    // narrow kernel: the caller's max_len hint; longer blocks are deferred (exact)
+#ifdef KVSEP_DIAG  // the round-1 in-kernel verify compare, kept for the sorted-window diag variants 24 / 25
+  const uint32_t* diag_expect;
+  unsigned long long* diag_first_bad;
+  unsigned long long* diag_nbad;
+#endif
   const DevTables* tabs;
 };
 
@@ -1188,7 +1193,9 @@ __device__ __forceinline__ void wave_sort64(uint32_t& key, uint32_t& idx, uint32
 // slot s takes the block at sorted position 8k + s (two ds_bpermutes to find it, four to fetch its descriptor).
 // The rows, the slot tree and the end path are the narrow kernel's (nstage / nfinish); blocks over the hint go to
 // narrow_deferred as there.
-template <int kG, bool kNT, int kThreads, bool kDrain = false>  // kDrain: diag, vmcnt(0) after each group's emit
+// kDrain: diag, vmcnt(0) after each group's emit.  kVIn (diag): 1 = the compare inside the kernel as before round 2
+// (load expected[b], compare, atomics); 2 = only the load of expected[b], folded into nothing
+template <int kG, bool kNT, int kThreads, bool kDrain = false, int kVIn = 0>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   constexpr uint32_t kPerGroup = 64 / kNarrowLanes;
@@ -1299,7 +1306,21 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesAr
           take_empty(ib, B);
         }
       });
-      if (j == kNarrowLanes - 1 && ia.live) emit_block(a, ia.w + ia.src, ~reg);
+      if (j == kNarrowLanes - 1 && ia.live) {
+        emit_block(a, ia.w + ia.src, ~reg);
+#ifdef KVSEP_DIAG
+        const uint64_t b = ia.w + ia.src;
+        if (kVIn == 1 && a.diag_expect && mask_crc(~reg) != a.diag_expect[b]) {
+          atomicMin(a.diag_first_bad, (unsigned long long)b);
+          atomicAdd(a.diag_nbad, 1ull);
+        }
+        if (kVIn == 2 && a.diag_expect) {
+          uint32_t z = 0;
+          asm volatile("" : "+v"(z));
+          a.out[b] = ~reg ^ (a.diag_expect[b] & z);
+        }
+#endif
+      }
       if (kDrain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (here) {
         ++k;
@@ -1824,6 +1845,14 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     KVSEP_HIP(hipMemsetAsync(first_bad, 0xff, 8, s));
     KVSEP_HIP(hipMemsetAsync(nbad, 0, 8, s));
   }
+#ifdef KVSEP_DIAG  // sorted-window variants 24 / 25 compare inside the kernel (no verify_finish_kernel pass)
+  const bool diag_vin = expect && (c->narrow == 24 || c->narrow == 25);
+  a.diag_expect = diag_vin ? expect : nullptr;
+  a.diag_first_bad = reinterpret_cast<unsigned long long*>(first_bad);
+  a.diag_nbad = reinterpret_cast<unsigned long long*>(nbad);
+#else
+  constexpr bool diag_vin = false;
+#endif
   if (count == 0) return KVSEP_OK;
   if (planned) {
     int rc = ensure_plan(sc, a.piece_bytes, count, total_bytes);
@@ -1888,6 +1917,8 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
       case 21: crc32c_narrow_sorted_kernel<4, true, 512><<<grid, 512, 0, s>>>(a); break;
       case 22: crc32c_narrow_sorted_kernel<4, true, 768><<<grid, 768, 0, s>>>(a); break;
       case 23: crc32c_narrow_sorted_kernel<4, true, 1024, true><<<grid, 1024, 0, s>>>(a); break;  // drain per group
+      case 24: crc32c_narrow_sorted_kernel<4, true, 1024, false, 1><<<grid, 1024, 0, s>>>(a); break;  // compare inside
+      case 25: crc32c_narrow_sorted_kernel<4, true, 1024, false, 2><<<grid, 1024, 0, s>>>(a); break;  // load inside
       // compact 80 KiB LDS image (two workgroups per CU): 30 / 34: 8-wave workgroups, two per CU, persistent (34:
       // fill overlapped); 31 / 35: one 8-block group per wave, grid over the whole batch (the dispatcher balances);
       // 32: two groups per wave; 33: 16-wave workgroups, one per CU (the conflict cost alone)
@@ -1932,7 +1963,7 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     crc32c_combine_kernel<<<unsigned((count + 255) / 256), 256, 0, s>>>(a);
     KVSEP_HIP(hipGetLastError());
   }
-  if (expect) {
+  if (expect && !diag_vin) {
     verify_finish_kernel<<<unsigned((count + 255) / 256), 256, 0, s>>>(
         out, expect, count, reinterpret_cast<unsigned long long*>(first_bad), reinterpret_cast<unsigned long long*>(nbad));
     KVSEP_HIP(hipGetLastError());
