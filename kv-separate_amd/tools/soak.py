@@ -3,8 +3,9 @@
 suite samples only sparsely -- up to 200 K blocks, length mixes (uniform, Zipf, around 4 KiB, tiny, mixed with
 long), any byte offset, overlapping blocks, random or no inits -- through every kernel choice (auto, wide, narrow16,
 narrow8, sorted), every hint kind (none, exact, loose, understated), three piece sizes, the verify form with
-corrupted expectations, and the host forms (pinned-staged span, pointer per block, a two-member device group) and
-a hipGraph-captured device call.  Every result is compared with the oracle on the same bytes; prints one line per case and
+corrupted expectations, the host forms (pinned-staged span, pointer per block, a two-member device group), a
+hipGraph-captured device call, and the SST forms (trailer words; the read check over a file image with planted bad
+trailers).  Every result is compared with the oracle on the same bytes; prints one line per case and
 a summary, exits non-zero on the first mismatch.  usage: soak.py [--seconds 240] [--seed N]
 tests/test_gpu_soak.py runs a fixed, seeded number of these cases (soak(seed, max_cases=...)) in the -m gpu suite."""
 import argparse
@@ -94,7 +95,9 @@ def soak(seed, seconds=None, max_cases=None, log=print, pool=POOL):
         exp = oracle.batch(host, off, ln, init, threads=8)
         d_init = torch.from_numpy(init.view(np.int32)).to(dev) if init is not None else None
         out = torch.zeros(n, dtype=torch.int32, device=dev)
-        form = str(rng.choice(["device", "device", "device", "host_span", "host_ptrs", "group", "graph"]))
+        form = str(rng.choice(["device", "device", "device", "host_span", "host_ptrs", "group", "graph", "sst"]))
+        if form == "sst" and n > 20000:
+            form = "device"
         verify = form == "device" and rng.random() < 0.4
         if form != "device":
             if form == "host_span":
@@ -106,6 +109,37 @@ def soak(seed, seconds=None, max_cases=None, log=print, pool=POOL):
                                       np.asarray(exp[k:], np.uint32)])
             elif form == "group":
                 got = group.batch_host_span(host, off, ln, init)
+            elif form == "sst":  # table/table_builder.cc:209-232 and table/format.cc:99-108 over a file image
+                types = rng.integers(0, 2, n).astype(np.uint8)
+                pos = np.zeros(n, np.uint64)
+                pos[1:] = np.cumsum(ln[:-1] + np.uint64(5), dtype=np.uint64)
+                pos += np.uint64(rng.integers(0, 16))
+                img = splitmix64_bytes(int(pos[-1] + ln[-1]) + 5, seed + cases, 0).copy()
+                img[(pos + ln).astype(np.int64)] = types
+                crc = oracle.batch(img, pos, ln + np.uint64(1))  # Value(block || type)
+                c64 = crc.astype(np.uint64)
+                stored = ((((c64 >> np.uint64(15)) | (c64 << np.uint64(17))) + np.uint64(0xA282EAD8))
+                          & np.uint64(0xFFFFFFFF))
+                for k in range(4):
+                    img[(pos + ln + np.uint64(1 + k)).astype(np.int64)] = ((stored >> np.uint64(8 * k)) & 0xFF).astype(np.uint8)
+                bad = rng.random(n) < 0.01
+                img[(pos[bad] + ln[bad] + np.uint64(1)).astype(np.int64)] ^= np.uint8(1)
+                d_img = torch.from_numpy(img).to(dev)
+                tw = torch.zeros(n, dtype=torch.int32, device=dev)
+                ctx.sst_trailers_device(d_img.data_ptr(), u64(pos), u64(ln), torch.from_numpy(types).to(dev), tw,
+                                        total_bytes=int(ln.sum()), max_len=max_len)
+                fb = torch.zeros(1, dtype=torch.int64, device=dev)
+                nb = torch.zeros(1, dtype=torch.int64, device=dev)
+                ctx.sst_verify_device(d_img.data_ptr(), u64(pos), u64(ln), out, fb, nb, total_bytes=int(ln.sum()),
+                                      max_len=max_len)
+                torch.cuda.synchronize()
+                got = out.cpu().numpy().view(np.uint32)
+                exp = crc
+                tw_ok = np.array_equal(tw.cpu().numpy().view(np.uint32), stored.astype(np.uint32))
+                want_fb = int(np.argmax(bad)) if bad.any() else -1
+                if not tw_ok or int(nb.item()) != int(bad.sum()) or (bad.any() and int(fb.item()) != want_fb):
+                    raise Mismatch(f"seed {seed}: case {cases + 1} sst: trailers {'ok' if tw_ok else 'WRONG'}, nbad "
+                                   f"{int(nb.item())} vs {int(bad.sum())}, first_bad {int(fb.item())} vs {want_fb}")
             else:  # graph: capture one device call, replay it twice
                 ctx.reserve(n, int(ln.sum()))
                 out = torch.zeros(n, dtype=torch.int32, device=dev)

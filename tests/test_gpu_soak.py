@@ -1,8 +1,8 @@
 """Seeded randomised parity sweep (kv-separate_amd/tools/soak.py, a fixed number of cases): random batch shapes --
 up to 200 K blocks, uniform / Zipf / ~4 KiB / tiny / mixed lengths, packed or overlapping offsets, random or no
 inits -- through every kernel choice, hint kind (none, exact, loose, understated), three piece sizes, the verify
-form with planted mismatches, the host-span, pointer-per-block and device-group host forms, and a hipGraph-captured
-device call; every result bit-exact against the oracle (util/crc32c.cc:276-377 restated) on the same bytes.
+form with planted mismatches, the host-span, pointer-per-block and device-group host forms, a hipGraph-captured
+device call and the SST trailer / read-check forms; every result bit-exact against the oracle (util/crc32c.cc:276-377 restated) on the same bytes.
 The time-bounded tool found the sorted-window verify bug of round 2; this keeps a slice of it in
 the suite."""
 import os
