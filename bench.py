@@ -10,7 +10,8 @@ config 3 of BASELINE.json, 65,536 x 1 MiB blocks (64 GiB) per GPU (`--config 3a`
   5   the 512 GiB vlog (524,288 x 1,048,609-B records) split over the N ranks (strong scaling): each rank owns
       8/N distinct 64 GiB slices; with more than one, every pass regenerates its slice in HBM at its true stream
       offset outside the timed region, so all 512 GiB checksummed are distinct data
-N > 1: one process per GPU (torchrun), each rank checksums its own shard; no data-path collective.
+N > 1: one process per GPU, each rank checksums its own shard; no data-path collective.  The ranks come from torchrun,
+or -- `bench.py --gpus N` with no WORLD_SIZE in the environment -- from bench.py itself (launch_ranks), over RCCL.
 
 Outside the timed region: RCCL all-gather of every rank's u32 results (4 B per block) and a check of EVERY block
 against the reference's whole-batch outputs (tests/golden/full_cfg*.u32, computed by the compiled util/crc32c.cc)
@@ -312,6 +313,43 @@ def live_pmc_traffic(args, timeout_s=240):
         shutil.rmtree(d, ignore_errors=True)
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` without an outside launcher: start N ranks of this script as child processes (one per GPU,
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, rendezvous on 127.0.0.1), wait for all of them
+    and return the worst exit status.  Runs before this process makes any GPU call (it never initialises the GPU, so
+    the children are plain subprocesses, not an exec).  A rank that fails takes the others down."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      start_new_session=True))
+    worst = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            rc = procs[r].poll()
+            if rc is None:
+                continue
+            live.discard(r)
+            if rc != 0:
+                log(f"[launcher] rank {r} exited {rc}; stopping the other ranks")
+                worst = worst or (rc if rc > 0 else 128 - rc)
+                for q in live:
+                    try:
+                        os.killpg(procs[q].pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+        time.sleep(0.2)
+    return worst
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -336,14 +374,44 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="CPU work per thread count (>= 1 pass)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--roundtrip-gib", type=float, default=4.0)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: each rank joins a gloo group, the ranks agree on the world "
+                         "size and rank 0 prints a JSON line with n_gpus / backend (tests/test_bench_launch.py)")
     ap.add_argument("--pmc-json", default=None,
                     help="PMC summary of the same config (default profiles/pmc_cfg<config>.json, written by "
                          "kv-separate_amd/tools/pmc_summary.py from separate rocprofv3 --pmc passes)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            # one process per GPU, started from here; nothing above touched the GPU (device_count does not)
+            if not (args.dry_run or os.environ.get("KVSEP_BENCH_SAME_DEVICE")) and torch.cuda.device_count() < args.gpus:
+                log(f"--gpus {args.gpus}: only {torch.cuda.device_count()} GPU(s) visible")
+                sys.exit(2)
+            sys.exit(launch_ranks(args.gpus))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        log(f"--gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}: refusing to report a line for a different "
+            f"number of ranks")
+        sys.exit(2)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        if os.environ.get("KVSEP_BENCH_DRYRUN_FAIL_RANK") == str(rank):  # launcher test: this rank dies at start
+            sys.exit(3)
+        if world > 1:
+            dist.init_process_group("gloo")
+            t = torch.tensor([world, rank], dtype=torch.int64)
+            seen = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+            dist.all_gather(seen, t)
+            ranks = sorted(int(x[1]) for x in seen)
+            assert ranks == list(range(world)) and all(int(x[0]) == world for x in seen), seen
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "world_size": world,
+                              "backend": dist.get_backend() if world > 1 else None}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if os.environ.get("KVSEP_BENCH_SAME_DEVICE"):  # rehearsal: every rank on cuda:0, gloo for results
@@ -599,6 +667,8 @@ def main():
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,
+            "world_size": world,
+            "backend": dist.get_backend() if dd else None,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),

@@ -163,6 +163,19 @@ int kvsep_sst_trailers_device(kvsep_crc32c_ctx* ctx, void* stream, const void* b
 int kvsep_sst_verify_device(kvsep_crc32c_ctx* ctx, void* stream, const void* file_base, const uint64_t* off,
                             const uint64_t* len, uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count,
                             uint64_t total_bytes, uint64_t max_len);
+/* Host-resident forms of the two above, for blocks the way TableBuilder::WriteRawBlock (table/table_builder.cc:209-232)
+ * and ReadBlock (table/format.cc:73-108) hold them: in host memory.  Both go through the pinned staging pipeline of
+ * the host forms; blocking.
+ *   trailers: block[i] / len[i] host pointers, types[i] the compression type byte; masked_out[i] =
+ *             Mask(Extend(Value(block_i), &types[i], 1)).
+ *   verify:   `file` is an SST file image in host memory ([block][type][trailer word] at each handle off[i] / len[i];
+ *             KVSEP_EINVAL if a handle leaves no room for its 5-byte trailer, format.cc:84-87); out[i] =
+ *             Value(block, len + 1); *first_bad = lowest i whose out[i] != Unmask(stored word) (UINT64_MAX if none),
+ *             *nbad their number -- each such block is what ReadBlock reports as "block checksum mismatch". */
+int kvsep_sst_trailers_host(kvsep_crc32c_ctx* ctx, const char* const* block, const uint64_t* len, const uint8_t* types,
+                            uint32_t* masked_out, uint64_t count);
+int kvsep_sst_verify_host(kvsep_crc32c_ctx* ctx, const char* file, uint64_t n, const uint64_t* off, const uint64_t* len,
+                          uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count);
 
 /* ---------------------------------------------------------------- several GPUs in one process
  * Blocks are independent, so a batch is cut into contiguous block ranges balanced by bytes and each range runs on

@@ -1194,7 +1194,9 @@ __device__ __forceinline__ void wave_sort64(uint32_t& key, uint32_t& idx, uint32
 // The rows, the slot tree and the end path are the narrow kernel's (nstage / nfinish); blocks over the hint go to
 // narrow_deferred as there.
 // kDrain: diag, vmcnt(0) after each group's emit.  kVIn (diag): 1 = the compare inside the kernel as before round 2
-// (load expected[b], compare, atomics); 2 = only the load of expected[b], folded into nothing
+// (load expected[b], compare, atomics); 2 = only the load of expected[b], folded into nothing; 3 / 4 = 1 plus s_nops /
+// a full s_waitcnt after the emit's join; 5 = 1 with a plain store in place of the atomics; 6 = the compare in full
+// EXEC (load, compare, ballot) with the atomics behind a wave-uniform branch (tools/sorted_vin_bisect.py)
 template <int kG, bool kNT, int kThreads, bool kDrain = false, int kVIn = 0>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
@@ -1310,10 +1312,11 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesAr
         emit_block(a, ia.w + ia.src, ~reg);
 #ifdef KVSEP_DIAG
         const uint64_t b = ia.w + ia.src;
-        if (kVIn == 1 && a.diag_expect && mask_crc(~reg) != a.diag_expect[b]) {
+        if ((kVIn == 1 || kVIn == 3 || kVIn == 4) && a.diag_expect && mask_crc(~reg) != a.diag_expect[b]) {
           atomicMin(a.diag_first_bad, (unsigned long long)b);
           atomicAdd(a.diag_nbad, 1ull);
         }
+        if (kVIn == 5 && a.diag_expect && mask_crc(~reg) != a.diag_expect[b]) *a.diag_first_bad = b;  // plain store
         if (kVIn == 2 && a.diag_expect) {
           uint32_t z = 0;
           asm volatile("" : "+v"(z));
@@ -1321,6 +1324,25 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesAr
         }
 #endif
       }
+#ifdef KVSEP_DIAG
+      if (kVIn == 3) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // wait states after the join
+      if (kVIn == 4) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      if (kVIn == 6 && a.diag_expect) {  // compare with no divergent region around it: load, compare, ballot in full EXEC
+        const bool mine = j == kNarrowLanes - 1 && ia.live;
+        const uint64_t b = mine ? ia.w + ia.src : 0;
+        const bool bad = mine && mask_crc(~reg) != a.diag_expect[b];
+        const uint64_t m = __builtin_amdgcn_ballot_w64(bad);
+        if (m) {  // wave-uniform
+          const uint32_t src = uint32_t(__builtin_ctzll(m));
+          const uint64_t fb = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(b >> 32)), int(src)))) << 32) |
+                              uint32_t(__builtin_amdgcn_readlane(int(uint32_t(b)), int(src)));
+          if (lane == 0) {
+            atomicMin(a.diag_first_bad, (unsigned long long)fb);
+            atomicAdd(a.diag_nbad, (unsigned long long)__builtin_popcountll(m));
+          }
+        }
+      }
+#endif
       if (kDrain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (here) {
         ++k;
@@ -1846,7 +1868,7 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     KVSEP_HIP(hipMemsetAsync(nbad, 0, 8, s));
   }
 #ifdef KVSEP_DIAG  // sorted-window variants 24 / 25 compare inside the kernel (no verify_finish_kernel pass)
-  const bool diag_vin = expect && (c->narrow == 24 || c->narrow == 25);
+  const bool diag_vin = expect && c->narrow >= 24 && c->narrow <= 29;
   a.diag_expect = diag_vin ? expect : nullptr;
   a.diag_first_bad = reinterpret_cast<unsigned long long*>(first_bad);
   a.diag_nbad = reinterpret_cast<unsigned long long*>(nbad);
@@ -1919,6 +1941,10 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
       case 23: crc32c_narrow_sorted_kernel<4, true, 1024, true><<<grid, 1024, 0, s>>>(a); break;  // drain per group
       case 24: crc32c_narrow_sorted_kernel<4, true, 1024, false, 1><<<grid, 1024, 0, s>>>(a); break;  // compare inside
       case 25: crc32c_narrow_sorted_kernel<4, true, 1024, false, 2><<<grid, 1024, 0, s>>>(a); break;  // load inside
+      case 26: crc32c_narrow_sorted_kernel<4, true, 1024, false, 3><<<grid, 1024, 0, s>>>(a); break;  // 24 + s_nops
+      case 27: crc32c_narrow_sorted_kernel<4, true, 1024, false, 4><<<grid, 1024, 0, s>>>(a); break;  // 24 + drain
+      case 28: crc32c_narrow_sorted_kernel<4, true, 1024, false, 5><<<grid, 1024, 0, s>>>(a); break;  // store, no atomics
+      case 29: crc32c_narrow_sorted_kernel<4, true, 1024, false, 6><<<grid, 1024, 0, s>>>(a); break;  // ballot compare
       // compact 80 KiB LDS image (two workgroups per CU): 30 / 34: 8-wave workgroups, two per CU, persistent (34:
       // fill overlapped); 31 / 35: one 8-block group per wave, grid over the whole batch (the dispatcher balances);
       // 32: two groups per wave; 33: 16-wave workgroups, one per CU (the conflict cost alone)

@@ -41,6 +41,7 @@ inline void put_le32(char* p, uint32_t v) {
 constexpr uint64_t kVlogHeader = 8;       // db/log_format.h:40
 constexpr uint64_t kLogBlock = 32768;     // db/log_format.h:30
 constexpr uint64_t kLogHeader = 7;        // db/log_format.h:33
+constexpr uint64_t kSstTrailer = 5;       // table/format.h:81 kBlockTrailerSize
 
 }  // namespace
 
@@ -217,6 +218,46 @@ int kvsep_log_frame_host(kvsep_crc32c_ctx* ctx, const char* const* payload, cons
     at[i] = h + kLogHeader;
   }
   return kvsep::host_copy_parallel(ctx, at.data(), src.data(), flen.data(), nf);  // the fragment bytes
+}
+
+int kvsep_sst_trailers_host(kvsep_crc32c_ctx* ctx, const char* const* block, const uint64_t* len, const uint8_t* types,
+                            uint32_t* masked_out, uint64_t count) {
+  if (!ctx || (count && (!block || !len || !types || !masked_out))) return KVSEP_EINVAL;
+  if (!count) return KVSEP_OK;
+  // Value(block) for every block in one batched call through the pinned staging, then the trailer's one-byte
+  // extension by the type and Mask on the host (table/table_builder.cc:222-225)
+  const int rc = kvsep_crc32c_batch_host(ctx, nullptr, block, len, masked_out, count);
+  if (rc) return rc;
+  for (uint64_t i = 0; i < count; ++i) {
+    const char t = char(types[i]);
+    masked_out[i] = kvsep_crc32c_mask(kvsep_crc32c_extend_host(masked_out[i], &t, 1));
+  }
+  return KVSEP_OK;
+}
+
+int kvsep_sst_verify_host(kvsep_crc32c_ctx* ctx, const char* file, uint64_t n, const uint64_t* off, const uint64_t* len,
+                          uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count) {
+  if (!ctx || (!file && n) || (count && (!off || !len || !out))) return KVSEP_EINVAL;
+  std::vector<uint64_t> len1(count);
+  for (uint64_t i = 0; i < count; ++i) {
+    // the handle must leave room for the 5-byte trailer (table/format.cc:84-87: "truncated block read")
+    if (off[i] > n || len[i] > n - off[i] || n - off[i] - len[i] < kSstTrailer) return KVSEP_EINVAL;
+    len1[i] = len[i] + 1;  // Value(data, n + 1): the block and its type byte (format.cc:102)
+  }
+  if (count) {
+    const int rc = kvsep_crc32c_batch_host_span(ctx, file, n, off, len1.data(), nullptr, out, count);
+    if (rc) return rc;
+  }
+  uint64_t fb = ~0ull, nb = 0;
+  for (uint64_t i = 0; i < count; ++i) {
+    if (out[i] != kvsep_crc32c_unmask(le32(file + off[i] + len[i] + 1))) {  // format.cc:101-106
+      if (fb == ~0ull) fb = i;
+      ++nb;
+    }
+  }
+  if (first_bad) *first_bad = fb;
+  if (nbad) *nbad = nb;
+  return KVSEP_OK;
 }
 
 uint64_t kvsep_log_accept(const uint64_t* off, const uint8_t* ok, uint64_t count, uint64_t n, uint8_t* accept) {

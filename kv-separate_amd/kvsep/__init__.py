@@ -99,6 +99,11 @@ _SIGS = {
     "kvsep_sst_verify_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]),
+    "kvsep_sst_trailers_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_uint64]),
+    "kvsep_sst_verify_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_uint64]),
     "kvsep_crc32c_partition": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]),
     "kvsep_crc32c_group_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "kvsep_crc32c_group_destroy": (None, [ctypes.c_void_p]),
@@ -422,6 +427,35 @@ class Context:
         _check(lib().kvsep_sst_verify_device(self._h, _stream_handle(stream), _dptr(file_base), _dptr(off),
                                              _dptr(length), _dptr(out), _dptr(first_bad), _dptr(nbad), count,
                                              total_bytes, max_len), "kvsep_sst_verify_device")
+
+    def sst_trailers(self, blocks, types):
+        """table/table_builder.cc:209-232 for host-resident blocks -> uint32 trailer words
+        Mask(Extend(Value(block), &type, 1)) (kvsep_sst_trailers_host)."""
+        keep = [_buf(b) for b in blocks]
+        k = len(blocks)
+        ptrs = (ctypes.c_void_p * max(k, 1))(*[x[0].value for x in keep])
+        lens = np.array([x[1].nbytes for x in keep], dtype=np.uint64)
+        t = np.ascontiguousarray(types, dtype=np.uint8)
+        out = np.zeros(max(k, 1), dtype=np.uint32)
+        _check(lib().kvsep_sst_trailers_host(self._h, ptrs, lens.ctypes.data_as(ctypes.c_void_p),
+                                             t.ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p), k),
+               "kvsep_sst_trailers_host")
+        return out[:k]
+
+    def sst_verify(self, image, off, length):
+        """table/format.cc:73-108 for every block handle (off, length) of a host SST file image -> (out, first_bad,
+        nbad): out[i] = Value(block, len + 1); first_bad = -1 when every block matches its stored trailer word."""
+        p, keep = _buf(image)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint64)
+        k = off.size
+        out = np.zeros(max(k, 1), dtype=np.uint32)
+        fb, nb = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().kvsep_sst_verify_host(self._h, p, keep.nbytes, off.ctypes.data_as(ctypes.c_void_p),
+                                           length.ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p),
+                                           ctypes.byref(fb), ctypes.byref(nb), k), "kvsep_sst_verify_host")
+        first = -1 if fb.value == 0xFFFFFFFFFFFFFFFF else fb.value
+        return out[:k], first, nb.value
 
 
 def vlog_walk(image):
