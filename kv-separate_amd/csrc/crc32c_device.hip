@@ -82,11 +82,11 @@ struct PiecesArgs {
                                     // 0: adaptive, clamp(total / (64 * nwaves), 4, 32)
   uint32_t guided_cap;              // dynamic schedule: at most this many items per grab (0: no cap)
   uint64_t hint;                    // narrow kernel: the caller's max_len hint; longer blocks are deferred (exact)
-#ifdef KVSEP_DIAG  // the round-1 in-kernel verify compare, kept for the sorted-window diag variants 24 / 25
-  const uint32_t* diag_expect;
-  unsigned long long* diag_first_bad;
-  unsigned long long* diag_nbad;
-#endif
+  // verify form (kVerify kernels): Mask(crc of block b) must equal expect[b]; mismatches post the lowest block index
+  // (atomicMin) and their number (atomicAdd) -- the check of db/value_log_reader.cc:109-122 / table/format.cc:99-106
+  const uint32_t* expect;
+  unsigned long long* first_bad;
+  unsigned long long* nbad;
   const DevTables* tabs;
 };
 
@@ -422,8 +422,44 @@ __device__ uint32_t gf2_shift(const DevTables* tabs, uint32_t reg, uint64_t n) {
   return gf2_mulmod(p, reg);
 }
 
-// The CRC kernels only store the result; the verify form's Mask/compare runs after them (verify_finish_kernel).
 __device__ __forceinline__ void emit_block(const PiecesArgs& a, uint64_t b, uint32_t crc) { a.out[b] = crc; }
+
+// The verify form fused into the CRC kernels (db/value_log_reader.cc:109-122, table/format.cc:99-106).  Called by the
+// whole wave (full EXEC) right after a group's emit: lanes with `mine` hold block b's crc and the stored word `ex`
+// they loaded before the next group's staging (so waiting for it never drains those loads).  The compare itself is
+// branch-free; the wave ballots the mismatches and only a mismatch enters a wave-uniform branch, where one lane posts
+// the wave's lowest mismatching index and the count.  A per-lane branch on the compare nested inside the emit's
+// divergent branch is what made the round-1 sorted-window kernel miscompute (diag variants 24-29).
+// The lane's block is base + idx (base wave-uniform): one VGPR for the index, not a 64-bit pair.
+__device__ __forceinline__ void verify_wave(const PiecesArgs& a, uint32_t lane, bool mine, uint64_t base, uint32_t idx,
+                                            uint32_t crc, uint32_t ex) {
+  const uint64_t m = __builtin_amdgcn_ballot_w64(mine && mask_crc(crc) != ex);
+  if (m) {  // wave-uniform
+    uint32_t best = ~0u;
+    for (uint64_t t = m; t; t &= t - 1) {
+      const uint32_t il = uint32_t(__builtin_amdgcn_readlane(int(idx), __builtin_ctzll(t)));
+      best = il < best ? il : best;
+    }
+    if (lane == 0) {
+      atomicMin(a.first_bad, (unsigned long long)(base + best));
+      atomicAdd(a.nbad, (unsigned long long)__builtin_popcountll(m));
+    }
+  }
+}
+
+// One block checked by a whole wave whose crc and stored word are wave-uniform (the wide kernel, the deferred walk).
+__device__ __forceinline__ void verify_uniform(const PiecesArgs& a, uint32_t lane, uint64_t b, uint32_t crc,
+                                               uint32_t ex) {
+  if (mask_crc(crc) != ex && lane == 0) {
+    atomicMin(a.first_bad, (unsigned long long)b);
+    atomicAdd(a.nbad, 1ull);
+  }
+}
+
+// A 32-bit global load (address space 1), for the stored words of the verify form.
+__device__ __forceinline__ uint32_t ld32(const uint32_t* p) {
+  return *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(reinterpret_cast<uintptr_t>(p));
+}
 
 // LDS image of a CRC workgroup: the replicated fold table `rep` (4 byte-tables) at [0, 128 KiB), then the
 // small tables (Z_4, the tree tables, the byte table) as one contiguous run.
@@ -555,8 +591,10 @@ __device__ __forceinline__ void fill_lds_compact(uint8_t* lds, const uint32_t* r
 
 // kThreads: 512 (8 waves, 2 per SIMD, <= 256 VGPRs; the default), 768, 1024 or 256 for A/B (launch_pieces_v).
 // One workgroup per CU in every case (the LDS image is 157 KiB).
+// kVerify: the verify form -- each whole block this kernel emits is checked against a.expect (verify_uniform); the
+// pieces of split blocks are checked by the combine kernel, which produces their CRC.
 template <bool kPlanned, bool kDynamic, int kG, bool kNT, bool kAhead, int kAbl = 0, int kThreads = kWgThreads,
-          bool kAlign = true>
+          bool kAlign = true, bool kVerify = false>
 __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -632,12 +670,12 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   // first-touch descriptor loads out of the per-item critical path (short blocks).
   uint64_t w0 = 0, wn = 0;        // window [w0, w0 + wn) of the current run
   uintptr_t w_ps = 0, w_pe = 0;   // per lane
-  uint32_t w_b = 0, w_reg0 = 0, w_only = 0;
+  uint32_t w_b = 0, w_reg0 = 0, w_only = 0, w_exp = 0;
   auto fill_set = [&](uint64_t start, uint64_t n, uintptr_t& w_ps, uintptr_t& w_pe, uint32_t& w_b, uint32_t& w_reg0,
-                      uint32_t& w_only) {
+                      uint32_t& w_only, uint32_t& w_exp) {
     const uint64_t g = start + lane;
     w_ps = w_pe = 0;
-    w_b = w_reg0 = w_only = 0;
+    w_b = w_reg0 = w_only = w_exp = 0;
     if (g < start + n) {
       uint64_t b, rs, re;
       bool first, only;
@@ -662,16 +700,17 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
       w_b = uint32_t(b);
       w_reg0 = first ? ~(a.init ? a.init[b] : 0u) : 0u;
       w_only = only ? 1u : 0u;
+      if (kVerify) w_exp = only ? a.expect[b] : 0u;  // travels with the descriptors, a window ahead of its use
     }
   };
   auto fill = [&](uint64_t start, uint64_t stop) {
     w0 = start;
     wn = stop - start < 64 ? stop - start : 64;
-    fill_set(w0, wn, w_ps, w_pe, w_b, w_reg0, w_only);
+    fill_set(w0, wn, w_ps, w_pe, w_b, w_reg0, w_only, w_exp);
   };
   struct Item {
     uint64_t g, b;
-    uint32_t reg0;
+    uint32_t reg0, exp;
     bool only;
   };
   auto take = [&](uint64_t g, Item& it, Staged<kG>& st) {  // item g of the window -> stage its loads
@@ -682,6 +721,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
     it.b = rl(w_b);
     it.reg0 = rl(w_reg0);
     it.only = rl(w_only) != 0;
+    it.exp = kVerify ? rl(w_exp) : 0u;
     const uintptr_t ps = (uintptr_t(rl(uint32_t(w_ps >> 32))) << 32) | uintptr_t(rl(uint32_t(w_ps)));
     const uintptr_t pe = (uintptr_t(rl(uint32_t(w_pe >> 32))) << 32) | uintptr_t(rl(uint32_t(w_pe)));
     stage<kG, kNT, kAlign>(st, ps, pe, lane, reinterpret_cast<uintptr_t>(a.tabs), vz);
@@ -691,6 +731,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
       if (it.only) emit_block(a, it.b, ~reg);
       else a.partial[it.g] = reg;
     }
+    // lane 0 holds the register: its readlane makes the compare, and the branch on it, wave-uniform
+    if (kVerify && it.only) verify_uniform(a, lane, it.b, ~uint32_t(__builtin_amdgcn_readlane(int(reg), 0)), it.exp);
   };
 
   // One item: finish item g (staged in A) while item g+1 is staged into B.  The loop below alternates the
@@ -945,10 +987,15 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
 // [lo, hi) again and checksums those blocks one at a time, each cut into parts of <= 1 GiB, 8 at a time (one per
 // slot; the slot geometry is 32-bit), merged with R(A||B) = Z_|B|(R(A)) ^ R(B) through gf2_shift.  Slower than the
 // main path (long blocks are not what the narrow kernels are for) but exact for any 64-bit length.
-template <int kG, bool kNT, bool kAlignN, typename Lay = LdsFull>
+template <int kG, bool kNT, bool kAlignN, typename Lay = LdsFull, bool kVerify = false>
 __device__ __forceinline__ void narrow_deferred(const PiecesArgs& a, const uint8_t* lds, uint64_t lo, uint64_t hi,
-                                                uint32_t lane, uint32_t lc0, uint32_t lc1, uintptr_t dummy) {
+                                                uintptr_t dummy) {
   constexpr uint32_t kPerGroup = 64 / kNarrowLanes;
+  // The lane constants are recomputed here (volatile, so not merged with the kernel's own): values kept live across
+  // the main group loop for this rarely taken walk would cost registers at the 16-wave kernels' 128-VGPR cap.
+  uint32_t lane;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+  const uint32_t lc0 = Lay::lc0(lane), lc1 = Lay::lc1(lane);
   const uint32_t j = lane & (kNarrowLanes - 1);
   const uint32_t slot = lane / kNarrowLanes;
   const uint32_t hint32 = uint32_t(a.hint);
@@ -1007,6 +1054,8 @@ __device__ __forceinline__ void narrow_deferred(const PiecesArgs& a, const uint8
             acc ^= uint32_t(__builtin_amdgcn_readlane(int(reg), int(t * kNarrowLanes + kNarrowLanes - 1)));
         }
         if (lane == 0) emit_block(a, g + k, ~acc);
+        // acc is wave-uniform (a readlane sum); so is the stored word, read through readfirstlane
+        if (kVerify) verify_uniform(a, lane, g + k, ~acc, uint32_t(__builtin_amdgcn_readfirstlane(int(ld32(a.expect + g + k)))));
       }
     }
   }
@@ -1015,8 +1064,10 @@ __device__ __forceinline__ void narrow_deferred(const PiecesArgs& a, const uint8
 // Unsplit batches only (every block <= 64 KiB <= piece_bytes); static contiguous runs of 8-block groups.
 // Lay: the LDS layout (LdsFull: one workgroup per CU; LdsCompact: two).  The runs follow gridDim, so a grid of more
 // workgroups than fit at once is the same computation (the hardware dispatcher then hands out the runs).
+// kVerify: the verify form (verify_wave after each group; the stored words are loaded just before the next group's
+// staging).
 template <int kG, bool kNT, int kThreads, bool kOverlap = false, int kAbl = 0, bool kAlignN = true,
-          typename Lay = LdsFull>
+          typename Lay = LdsFull, bool kVerify = false>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   __shared__ __attribute__((aligned(16))) uint8_t lds[Lay::kBytes];
@@ -1096,9 +1147,24 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     const uint64_t gn = g + kPerGroup;
     // the next group is staged inside nfinish, after this group's last row loads; unconditional (past the
     // end it is an empty group of dummy loads: see the wide kernel's step())
+    uint32_t ex = 0;
     const uint32_t reg = nfinish<kG, kNT, kAbl, kAlignN, Lay>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
-                                                           [&]() { take(gn, ib, B); });
-    if (j == kNarrowLanes - 1 && g + slot < hi && !ia.over) emit_block(a, g + slot, ~reg);
+                                                           [&]() {
+                                                             if (kVerify) {  // this group's stored words, issued
+                                                               // before the next group's loads (see verify_wave);
+                                                               // uniform base + 32-bit lane offset (clamped in range)
+                                                               const uint64_t last = hi - 1 - g;
+                                                               const uint32_t sl = slot < last ? slot : uint32_t(last);
+                                                               ex = ld32(a.expect + g + sl);
+                                                               __builtin_amdgcn_sched_barrier(0);
+                                                             }
+                                                             take(gn, ib, B);
+                                                           });
+    const bool mine = j == kNarrowLanes - 1 && g + slot < hi && !ia.over;
+    // compare before the store: a store between the stored word's load and its wait (in a branch the wait must also
+    // cover when skipped) would make that wait one count short and hold up the next group's first staged load
+    if (kVerify) verify_wave(a, lane, mine, g, slot, ~reg, ex);
+    if (mine) emit_block(a, g + slot, ~reg);
     load_desc(gn + kPerGroup, dn);  // here, where this group's registers are dead
     return gn < hi;
   };
@@ -1163,7 +1229,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   KVSEP_NSTAMP(7);
 #undef KVSEP_NSTEP
 #undef KVSEP_NSTAMP
-  if (deferred) narrow_deferred<kG, kNT, kAlignN, Lay>(a, lds, lo, hi, lane, lc0, lc1, dummy);
+  if (deferred) narrow_deferred<kG, kNT, kAlignN, Lay, kVerify>(a, lds, lo, hi, dummy);
 }
 
 // Bitonic sort of one (key, idx) pair per lane over the wavefront, ascending by key (ties by idx, so the two
@@ -1197,7 +1263,7 @@ __device__ __forceinline__ void wave_sort64(uint32_t& key, uint32_t& idx, uint32
 // (load expected[b], compare, atomics); 2 = only the load of expected[b], folded into nothing; 3 / 4 = 1 plus s_nops /
 // a full s_waitcnt after the emit's join; 5 = 1 with a plain store in place of the atomics; 6 = the compare in full
 // EXEC (load, compare, ballot) with the atomics behind a wave-uniform branch (tools/sorted_vin_bisect.py)
-template <int kG, bool kNT, int kThreads, bool kDrain = false, int kVIn = 0>
+template <int kG, bool kNT, int kThreads, bool kDrain = false, int kVIn = 0, bool kVerify = false>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   constexpr uint32_t kPerGroup = 64 / kNarrowLanes;
@@ -1298,6 +1364,13 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesAr
     auto step = [&](NItem& ia, NStaged<kG>& A, NItem& ib, NStaged<kG>& B) -> bool {
       const bool here = k + 1 < nk;
       const bool next_win = !here && Wn < hi;
+      // the verify form: this group's stored words, issued before the group's remaining row loads and the next group's
+      // staging, from one place on every path (so the wait for them is a counted vmcnt, never a drain; see verify_wave)
+      uint32_t ex = 0;
+      if (kVerify) {
+        ex = ld32(a.expect + ia.w + (ia.live ? ia.src : 0u));
+        __builtin_amdgcn_sched_barrier(0);
+      }
       const uint32_t reg = nfinish<kG, kNT, 0, true>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy, [&]() {
         if (here) {
           take(W, cw, k + 1, ib, B);
@@ -1308,37 +1381,38 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesAr
           take_empty(ib, B);
         }
       });
+      if (kVerify) verify_wave(a, lane, j == kNarrowLanes - 1 && ia.live, ia.w, ia.src, ~reg, ex);  // before the store
       if (j == kNarrowLanes - 1 && ia.live) {
         emit_block(a, ia.w + ia.src, ~reg);
 #ifdef KVSEP_DIAG
         const uint64_t b = ia.w + ia.src;
-        if ((kVIn == 1 || kVIn == 3 || kVIn == 4) && a.diag_expect && mask_crc(~reg) != a.diag_expect[b]) {
-          atomicMin(a.diag_first_bad, (unsigned long long)b);
-          atomicAdd(a.diag_nbad, 1ull);
+        if ((kVIn == 1 || kVIn == 3 || kVIn == 4) && a.expect && mask_crc(~reg) != a.expect[b]) {
+          atomicMin(a.first_bad, (unsigned long long)b);
+          atomicAdd(a.nbad, 1ull);
         }
-        if (kVIn == 5 && a.diag_expect && mask_crc(~reg) != a.diag_expect[b]) *a.diag_first_bad = b;  // plain store
-        if (kVIn == 2 && a.diag_expect) {
+        if (kVIn == 5 && a.expect && mask_crc(~reg) != a.expect[b]) *a.first_bad = b;  // plain store
+        if (kVIn == 2 && a.expect) {
           uint32_t z = 0;
           asm volatile("" : "+v"(z));
-          a.out[b] = ~reg ^ (a.diag_expect[b] & z);
+          a.out[b] = ~reg ^ (a.expect[b] & z);
         }
 #endif
       }
 #ifdef KVSEP_DIAG
       if (kVIn == 3) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // wait states after the join
       if (kVIn == 4) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      if (kVIn == 6 && a.diag_expect) {  // compare with no divergent region around it: load, compare, ballot in full EXEC
+      if (kVIn == 6 && a.expect) {  // compare with no divergent region around it: load, compare, ballot in full EXEC
         const bool mine = j == kNarrowLanes - 1 && ia.live;
         const uint64_t b = mine ? ia.w + ia.src : 0;
-        const bool bad = mine && mask_crc(~reg) != a.diag_expect[b];
+        const bool bad = mine && mask_crc(~reg) != a.expect[b];
         const uint64_t m = __builtin_amdgcn_ballot_w64(bad);
         if (m) {  // wave-uniform
           const uint32_t src = uint32_t(__builtin_ctzll(m));
           const uint64_t fb = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(b >> 32)), int(src)))) << 32) |
                               uint32_t(__builtin_amdgcn_readlane(int(uint32_t(b)), int(src)));
           if (lane == 0) {
-            atomicMin(a.diag_first_bad, (unsigned long long)fb);
-            atomicAdd(a.diag_nbad, (unsigned long long)__builtin_popcountll(m));
+            atomicMin(a.first_bad, (unsigned long long)fb);
+            atomicAdd(a.nbad, (unsigned long long)__builtin_popcountll(m));
           }
         }
       }
@@ -1362,24 +1436,32 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesAr
       if (!step(nxt, T, cur, S)) break;
     }
   }
-  if (deferred) narrow_deferred<kG, kNT, true>(a, lds, lo, hi, lane, lc0, lc1, dummy);
+  if (deferred) narrow_deferred<kG, kNT, true, LdsFull, kVerify>(a, lds, lo, hi, dummy);
 }
 
-// One thread per block: Horner over the block's pieces, R <- Z_piece(R) ^ R_piece.
+// One thread per block: Horner over the block's pieces, R <- Z_piece(R) ^ R_piece.  kVerify: also the verify form's
+// compare for the split blocks (the CRC kernel checked the whole ones).
+template <bool kVerify = false>
 __global__ void __launch_bounds__(256) crc32c_combine_kernel(PiecesArgs a) {
   __shared__ uint32_t zp[1024];
   for (uint32_t i = threadIdx.x; i < 1024; i += 256) zp[i] = a.zpiece[i];
   __syncthreads();
   const uint64_t b = uint64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (b >= a.count) return;
-  const uint64_t s = a.pstart[b], e = a.pstart[b + 1];
-  if (e - s <= 1 || a.pstart[a.count] > a.max_pieces) return;  // unsplit fallback: already emitted
-  uint32_t acc = a.partial[s];
-  for (uint64_t g = s + 1; g < e; ++g) {
-    acc = zp[acc & 255u] ^ zp[256 + ((acc >> 8) & 255u)] ^ zp[512 + ((acc >> 16) & 255u)] ^ zp[768 + (acc >> 24)];
-    acc ^= a.partial[g];
+  const uint64_t bb = b < a.count ? b : a.count - 1;
+  const uint64_t s = a.pstart[bb], e = a.pstart[bb + 1];
+  // unsplit blocks (and the unsplit fallback) were emitted -- and checked -- by the CRC kernel
+  const bool mine = b < a.count && e - s > 1 && a.pstart[a.count] <= a.max_pieces;
+  uint32_t crc = 0;
+  if (mine) {
+    uint32_t acc = a.partial[s];
+    for (uint64_t g = s + 1; g < e; ++g) {
+      acc = zp[acc & 255u] ^ zp[256 + ((acc >> 8) & 255u)] ^ zp[512 + ((acc >> 16) & 255u)] ^ zp[768 + (acc >> 24)];
+      acc ^= a.partial[g];
+    }
+    crc = ~acc;
+    emit_block(a, b, crc);
   }
-  emit_block(a, b, ~acc);
+  if (kVerify) verify_wave(a, threadIdx.x & 63u, mine, uint64_t(blockIdx.x) * 256, threadIdx.x, crc, ld32(a.expect + bb));
 }
 
 __global__ void crc32c_plan_count_kernel(const uint64_t* len, uint64_t count, uint64_t piece_bytes,
@@ -1393,11 +1475,9 @@ __global__ void crc32c_plan_count_kernel(const uint64_t* len, uint64_t count, ui
   counts[b] = n < 2 * piece_bytes ? 1u : n / piece_bytes;
 }
 
-// Verify form: the Mask/compare of db/value_log_reader.cc:109-122 (and table/format.cc:102-106) as one pass over
-// the u32 results after the CRC kernels, never inside them.  Inside a kernel's pipeline the compare's load of
-// expect[b] drained every staged load of the next item (vmcnt(0)) at each block, and with the compare there the
-// sorted-window kernel returned wrong CRCs from the third group of a window on (found by tools/soak.py; DESIGN
-// §3.2).  Wave-level reduction: one atomicMin / atomicAdd per wave that saw a mismatch.
+// Verify form as a separate pass over the u32 results: only for the A/B variants of the KVSEP_DIAG tools build, whose
+// kernels have no fused compare (the shipped kernels compare in place: verify_wave / verify_uniform).  Wave-level
+// reduction: one atomicMin / atomicAdd per wave that saw a mismatch.
 __global__ void __launch_bounds__(256) verify_finish_kernel(const uint32_t* out, const uint32_t* expect,
                                                             uint64_t count, unsigned long long* first_bad,
                                                             unsigned long long* nbad) {
@@ -1756,7 +1836,7 @@ hipEvent_t take_event(kvsep_crc32c_ctx* c) {
   return e;
 }
 
-template <bool P, bool D>
+template <bool P, bool D, bool V>
 void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs& a) {
   // Default (1): 8-wave workgroups (2 waves per SIMD, up to 256 VGPRs), 4-row groups, non-temporal loads, next
   // item staged ahead.  On one MI355X, interleaved in one process (tools/ab_variants.py), 8 waves beat 16 waves
@@ -1772,6 +1852,10 @@ void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs
   // Only the default is compiled into the shipped library; the rest exist in the KVSEP_DIAG tools build
   // (`make -C kv-separate_amd diag` -> tools/libkvsep_diag.so).
   constexpr int T = kWgThreads;
+  if (V) {  // the verify form: the shipped configuration only
+    crc32c_pieces_kernel<P, D, 4, true, true, 0, T, true, true><<<grid, T, 0, s>>>(a);
+    return;
+  }
   switch (variant) {
 #ifdef KVSEP_DIAG
     case 0: crc32c_pieces_kernel<P, D, 4, false, true, 0, T><<<grid, T, 0, s>>>(a); break;
@@ -1808,14 +1892,21 @@ void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs
   }
 }
 
-void launch_pieces(bool planned, bool dyn, int variant, unsigned grid, hipStream_t s, const PiecesArgs& a) {
+template <bool V>
+void launch_pieces_vv(bool planned, bool dyn, int variant, unsigned grid, hipStream_t s, const PiecesArgs& a) {
   if (planned) {
-    if (dyn) launch_pieces_v<true, true>(variant, grid, s, a);
-    else launch_pieces_v<true, false>(variant, grid, s, a);
+    if (dyn) launch_pieces_v<true, true, V>(variant, grid, s, a);
+    else launch_pieces_v<true, false, V>(variant, grid, s, a);
   } else {
-    if (dyn) launch_pieces_v<false, true>(variant, grid, s, a);
-    else launch_pieces_v<false, false>(variant, grid, s, a);
+    if (dyn) launch_pieces_v<false, true, V>(variant, grid, s, a);
+    else launch_pieces_v<false, false, V>(variant, grid, s, a);
   }
+}
+
+void launch_pieces(bool planned, bool dyn, bool verify, int variant, unsigned grid, hipStream_t s,
+                   const PiecesArgs& a) {
+  if (verify) launch_pieces_vv<true>(planned, dyn, variant, grid, s, a);
+  else launch_pieces_vv<false>(planned, dyn, variant, grid, s, a);
 }
 
 int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* base, const uint64_t* off,
@@ -1867,14 +1958,12 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     KVSEP_HIP(hipMemsetAsync(first_bad, 0xff, 8, s));
     KVSEP_HIP(hipMemsetAsync(nbad, 0, 8, s));
   }
-#ifdef KVSEP_DIAG  // sorted-window variants 24 / 25 compare inside the kernel (no verify_finish_kernel pass)
-  const bool diag_vin = expect && c->narrow >= 24 && c->narrow <= 29;
-  a.diag_expect = diag_vin ? expect : nullptr;
-  a.diag_first_bad = reinterpret_cast<unsigned long long*>(first_bad);
-  a.diag_nbad = reinterpret_cast<unsigned long long*>(nbad);
-#else
-  constexpr bool diag_vin = false;
-#endif
+  a.expect = expect;
+  a.first_bad = reinterpret_cast<unsigned long long*>(first_bad);
+  a.nbad = reinterpret_cast<unsigned long long*>(nbad);
+  // The verify form's compare runs inside the CRC kernels (and the combine kernel for split blocks): `fused`.  Only
+  // the A/B variants of the KVSEP_DIAG tools build fall back to the separate verify_finish_kernel pass.
+  bool fused = true;
   if (count == 0) return KVSEP_OK;
   if (planned) {
     int rc = ensure_plan(sc, a.piece_bytes, count, total_bytes);
@@ -1924,6 +2013,15 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     if (c->narrow != 1 && c->narrow != 7 && c->kernel < 3) nv = c->narrow;
 #endif
     a.hint = max_len;
+    if (expect && (nv == 6 || nv == 9 || nv == 20)) {  // the verify form of the shipped narrow forms
+      switch (nv) {
+        case 9: crc32c_narrow_kernel<4, true, 512, true, 0, true, LdsFull, true><<<grid, 512, 0, s>>>(a); break;
+        case 20: crc32c_narrow_sorted_kernel<4, true, 1024, false, 0, true><<<grid, 1024, 0, s>>>(a); break;
+        default: crc32c_narrow_kernel<4, true, 1024, false, 0, true, LdsFull, true><<<grid, 1024, 0, s>>>(a); break;
+      }
+    } else {
+    // diag variants 24-29 run their own in-kernel compare; every other diag variant gets verify_finish_kernel
+    fused = !expect || (nv >= 24 && nv <= 29);
     switch (nv) {
 #ifdef KVSEP_DIAG
       case 2: crc32c_narrow_kernel<4, true, 512><<<grid, 512, 0, s>>>(a); break;
@@ -1977,8 +2075,9 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
       case 20: crc32c_narrow_sorted_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
       default: crc32c_narrow_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
     }
+    }
   } else {
-    launch_pieces(planned, dyn, c->variant, grid, s, a);
+    launch_pieces(planned, dyn, expect != nullptr, c->variant, grid, s, a);
   }
   KVSEP_HIP(hipGetLastError());
   if (c->timing && e0 && e1) {
@@ -1986,10 +2085,11 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     c->ev_pending.emplace_back(e0, e1);
   }
   if (planned) {
-    crc32c_combine_kernel<<<unsigned((count + 255) / 256), 256, 0, s>>>(a);
+    if (expect) crc32c_combine_kernel<true><<<unsigned((count + 255) / 256), 256, 0, s>>>(a);
+    else crc32c_combine_kernel<false><<<unsigned((count + 255) / 256), 256, 0, s>>>(a);
     KVSEP_HIP(hipGetLastError());
   }
-  if (expect && !diag_vin) {
+  if (expect && !fused) {
     verify_finish_kernel<<<unsigned((count + 255) / 256), 256, 0, s>>>(
         out, expect, count, reinterpret_cast<unsigned long long*>(first_bad), reinterpret_cast<unsigned long long*>(nbad));
     KVSEP_HIP(hipGetLastError());

@@ -25,6 +25,7 @@ Exit status 1 if any violation is found (the CPU test tests/test_kernel_resource
 import argparse
 import re
 import sys
+import zlib
 
 REG_RE = re.compile(r'\b([vs])\[(\d+):(\d+)\]|\b([vs])(\d+)\b|\b(vcc|exec|m0|scc)\b')
 
@@ -313,7 +314,7 @@ def audit(blocks, succ, model):
 
 # ------------------------------------------------------------------------------------------------------------------
 # EXEC model: concrete 64-bit masks.  Every per-lane compare (v_cmp) yields a pseudo-random lane mask fixed per
-# instruction; s_cselect of -1/0 and other scalar results are wave-uniform (all ones).  Mask arithmetic on SGPR pairs,
+# instruction text; s_cselect of -1/0 and other scalar results are wave-uniform (all ones).  Mask arithmetic on SGPR pairs,
 # VCC and EXEC (s_and/or/xor/andn2/orn2/mov and the *_saveexec forms) is evaluated exactly, so the structurizer's
 # if / else / flow sequences restore EXEC to the entry mask exactly where the program really is uniform again.  At a
 # join, a register whose incoming values differ becomes unknown (None).
@@ -364,7 +365,8 @@ def exec_step(state, k):
     op = k.op
     ops = [o.strip() for o in k.text.split(None, 1)[1].split(',')] if ' ' in k.text else []
     if op.startswith('v_cmp_') or op.startswith('v_cmpx_'):
-        v = _rand(k.line)
+        # keyed by the instruction text: the tail-duplicated copies of one compare (same registers) give one mask
+        v = _rand(zlib.crc32(k.text.encode()))
         if ex is not None:
             v &= ex
         if op.endswith('_e32') or op.startswith('v_cmpx_'):
@@ -429,11 +431,20 @@ def exec_step(state, k):
     return ex
 
 
-def _merge_masks(a, b):
+def _merge_masks(a, b, where=0):
+    """Join of two mask states.  EXEC that differs becomes unknown (the structurizer restores it from a saved mask
+    right after the join, see exec_step); any other lane mask that differs (a divergent boolean carried across the
+    join, e.g. `live`) becomes a phi: a fresh partial mask fixed per (join block, register), so later arithmetic on
+    it stays consistent from one trip of a loop to the next."""
     out = {}
     for key in set(a) | set(b):
         va, vb = a.get(key, None), b.get(key, None)
-        out[key] = va if va == vb else None
+        if va == vb:
+            out[key] = va
+        elif key == 'exec':
+            out[key] = None
+        else:
+            out[key] = _rand(zlib.crc32(('%d:%s' % (where, key)).encode()))
     return out
 
 
@@ -451,7 +462,7 @@ def exec_audit(blocks, succ):
         for k in blocks[i][1]:
             exec_step(st, k)
         for s in succ[i]:
-            m = dict(st) if ins[s] is None else _merge_masks(ins[s], st)
+            m = dict(st) if ins[s] is None else _merge_masks(ins[s], st, s)
             if ins[s] is None or m != ins[s]:
                 ins[s] = m
                 work.append(s)
@@ -472,10 +483,12 @@ def exec_audit(blocks, succ):
 CROSS = ('ds_bpermute', 'ds_permute', 'ds_swizzle', 'v_permlane')
 
 
-def crosslane_partial(blocks, succ):
+def crosslane_partial(blocks, succ, unknown=False):
+    """Cross-lane data ops executed under a partial EXEC (with unknown=True also those whose EXEC the model lost
+    track of -- at joins of tail-duplicated regions that carry lane-mask phis it does)."""
     hits = []
     for lab, k, ex in exec_audit(blocks, succ):
-        if ex == ALL:
+        if ex == ALL or (ex is None and not unknown):
             continue
         if k.op.startswith(CROSS) or '_dpp' in k.op or 'row_shr' in k.text or 'quad_perm' in k.text or \
                 'row_bcast' in k.text or 'row_ror' in k.text or 'wave_sh' in k.text or 'wave_ro' in k.text:
@@ -506,6 +519,7 @@ def main():
     ap.add_argument('--vm-model', default='inorder', choices=('inorder', 'loads'))
     ap.add_argument('-v', action='store_true')
     ap.add_argument('--crosslane', action='store_true', help='also list cross-lane ops under a partial EXEC')
+    ap.add_argument('--unknown', action='store_true', help='with --crosslane: also those under an EXEC the model lost')
     args = ap.parse_args()
     bad = 0
     nk = 0
@@ -524,7 +538,7 @@ def main():
             bad += 1
             print('%s:%d: %s of pending %s %s: %s' % (name, insn.line, how, r, ents, insn.text))
         if args.crosslane:
-            for lab, k, ex in crosslane_partial(blocks, succ):
+            for lab, k, ex in crosslane_partial(blocks, succ, args.unknown):
                 bad += 1
                 print('%s:%d: cross-lane data op under %s EXEC (%s): %s' % (name, k.line, 'unknown' if ex is None else
                                                                              'partial', lab, k.text))
