@@ -1147,19 +1147,17 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     const uint64_t gn = g + kPerGroup;
     // the next group is staged inside nfinish, after this group's last row loads; unconditional (past the
     // end it is an empty group of dummy loads: see the wide kernel's step())
+    // the verify form: this group's stored words (uniform base + a clamped 32-bit lane offset), issued before the
+    // group's remaining row loads and the next group's staging, so their latency hides under the group and the wait
+    // for them is a counted vmcnt (see verify_wave)
     uint32_t ex = 0;
+    if (kVerify) {
+      const uint64_t last = hi - 1 - g;
+      ex = ld32(a.expect + g + (slot < last ? slot : uint32_t(last)));
+      __builtin_amdgcn_sched_barrier(0);
+    }
     const uint32_t reg = nfinish<kG, kNT, kAbl, kAlignN, Lay>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
-                                                           [&]() {
-                                                             if (kVerify) {  // this group's stored words, issued
-                                                               // before the next group's loads (see verify_wave);
-                                                               // uniform base + 32-bit lane offset (clamped in range)
-                                                               const uint64_t last = hi - 1 - g;
-                                                               const uint32_t sl = slot < last ? slot : uint32_t(last);
-                                                               ex = ld32(a.expect + g + sl);
-                                                               __builtin_amdgcn_sched_barrier(0);
-                                                             }
-                                                             take(gn, ib, B);
-                                                           });
+                                                           [&]() { take(gn, ib, B); });
     const bool mine = j == kNarrowLanes - 1 && g + slot < hi && !ia.over;
     // compare before the store: a store between the stored word's load and its wait (in a branch the wait must also
     // cover when skipped) would make that wait one count short and hold up the next group's first staged load
@@ -1489,6 +1487,14 @@ __global__ void __launch_bounds__(256) verify_finish_kernel(const uint32_t* out,
   if (lane == uint32_t(__builtin_ctzll(m))) {  // the wave's first bad block is its lowest bad index
     atomicMin(first_bad, (unsigned long long)b);
     atomicAdd(nbad, (unsigned long long)__builtin_popcountll(m));
+  }
+}
+
+// The verify form's result words before the CRC kernels post to them: first_bad = UINT64_MAX, nbad = 0.
+__global__ void __launch_bounds__(64) verify_init_kernel(unsigned long long* first_bad, unsigned long long* nbad) {
+  if (threadIdx.x == 0) {
+    *first_bad = ~0ull;
+    *nbad = 0;
   }
 }
 
@@ -1955,8 +1961,10 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
       first_bad = reinterpret_cast<uint64_t*>(sc.d_verify);
       nbad = reinterpret_cast<uint64_t*>(sc.d_verify + 1);
     }
-    KVSEP_HIP(hipMemsetAsync(first_bad, 0xff, 8, s));
-    KVSEP_HIP(hipMemsetAsync(nbad, 0, 8, s));
+    // one tiny launch for both words (two memset nodes cost two launches of the graph / stream)
+    verify_init_kernel<<<1, 64, 0, s>>>(reinterpret_cast<unsigned long long*>(first_bad),
+                                        reinterpret_cast<unsigned long long*>(nbad));
+    KVSEP_HIP(hipGetLastError());
   }
   a.expect = expect;
   a.first_bad = reinterpret_cast<unsigned long long*>(first_bad);

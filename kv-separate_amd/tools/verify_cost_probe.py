@@ -4,7 +4,8 @@
 For each config the same device-resident batch is checksummed K times by kvsep_crc32c_batch_device and K times by
 kvsep_crc32c_verify_device (correct stored words, so nbad = 0), each as ONE hipGraph of K back-to-back calls timed with
 a HIP event pair on the replay stream, interleaved over several rounds in one process; the median per-call time of each
-form is reported.  Every verify call's results are checked (out == the batch form's, nbad == 0), and a last verify call
+form is reported (whole call: the verify form adds one tiny init launch for its two result words), and the CRC kernel
+alone (the library's event pair around it, eager launches).  Every verify call's results are checked (out == the batch form's, nbad == 0), and a last verify call
 with three planted bad words must report them.  Configs: 2 (65,536 x 4 KiB: the narrow kernel), 3b (65,536 vlog records
 of 1,048,609 B: the wide kernel + combine), 4s (config 4's blocks <= 32 KiB: the sorted-window kernel).
 usage: verify_cost_probe.py [--configs 2,3b,4s] [--steps 20] [--rounds 5]"""
@@ -95,6 +96,17 @@ for cfg in args.configs.split(","):
             e1.record()
             torch.cuda.synchronize()
             times[name].append(e0.elapsed_time(e1) * 1e3 / args.steps)  # us per call
+    # kernel-only: the library's HIP event pair around the main CRC kernel, eager launches (verify vs batch)
+    kern = {}
+    for name, fn in (("batch", batch_call), ("verify", verify_call)):
+        ctx.get_timing()
+        ctx.set_timing(True)
+        for _ in range(args.steps):
+            fn(torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        ctx.set_timing(False)
+        ms, nl = ctx.get_timing()
+        kern[name] = ms * 1e3 / max(1, nl)
     ok = np.array_equal(out_v.cpu().numpy(), out_b.cpu().numpy()) and int(nb.item()) == 0 and int(fb.item()) == -1
     bad = stored.copy()
     plant = [n // 3, n // 3 + 1, n - 1]
@@ -106,7 +118,9 @@ for cfg in args.configs.split(","):
     caught = (int(fb.item()), int(nb.item())) == (plant[0], len(plant))
     mb, mv = statistics.median(times["batch"]), statistics.median(times["verify"])
     results[cfg] = {"kernel": kname, "blocks": n, "bytes": tb, "batch_us": round(mb, 2), "verify_us": round(mv, 2),
-                    "verify_over_batch": round(mv / mb, 4), "batch_runs_us": [round(t, 2) for t in times["batch"]],
+                    "verify_over_batch": round(mv / mb, 4),
+                    "kernel_batch_us": round(kern["batch"], 2), "kernel_verify_us": round(kern["verify"], 2),
+                    "kernel_verify_over_batch": round(kern["verify"] / kern["batch"], 4), "batch_runs_us": [round(t, 2) for t in times["batch"]],
                     "verify_runs_us": [round(t, 2) for t in times["verify"]], "verify_exact": ok,
                     "planted_bad_caught": caught}
     print(json.dumps({cfg: results[cfg]}), flush=True)
