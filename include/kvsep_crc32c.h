@@ -27,6 +27,13 @@
 extern "C" {
 #endif
 
+/* ABI version.  2 (round 3): kvsep_vlog_verify_host takes *drop_bytes (7 arguments) and kvsep_crc32c_kernel_name
+ * takes total_bytes before max_len -- both changed in place from ABI 1, so a caller built against ABI 1 must be
+ * rebuilt; check kvsep_abi_version() == KVSEP_ABI_VERSION once at startup.  The reference's C++ symbol
+ * leveldb::crc32c::Extend is not in this library: it is in the libkvsep_leveldb_abi.so shim. */
+#define KVSEP_ABI_VERSION 2
+int kvsep_abi_version(void);
+
 #define KVSEP_OK 0
 #define KVSEP_EINVAL (-1)  /* bad argument */
 #define KVSEP_EHIP (-2)    /* a HIP runtime call failed (message via kvsep_last_error) */

@@ -1,6 +1,6 @@
 // kvsep_leveldb_crc32c.h -- stand-in for the reference's util/crc32c.h (util/crc32c.h:11-41): same
 // namespace, same declarations, same inline helpers.  Extend is declared, not defined, exactly as in
-// util/crc32c.h:17: libkvsep_crc32c.so exports the out-of-line definition (csrc/leveldb_abi.cpp), so a
+// util/crc32c.h:17: libkvsep_leveldb_abi.so exports the out-of-line definition (csrc/leveldb_abi.cpp), so a
 // KVDB build can either keep its own util/crc32c.h or include this one -- both resolve
 // leveldb::crc32c::Extend to the library at link time once util/crc32c.cc is dropped from the sources.
 // Call sites: db/value_log_writer.cc:57, db/value_log_reader.cc:110, db/log_writer.cc:19,98,
@@ -17,7 +17,7 @@ namespace leveldb {
 namespace crc32c {
 
 // util/crc32c.h:17 -- crc32c of concat(A, data[0,n-1]) where init_crc = crc32c(A).  Defined in
-// libkvsep_crc32c.so (C++ linkage, = kvsep_crc32c_extend).
+// libkvsep_leveldb_abi.so (C++ linkage, = kvsep_crc32c_extend of libkvsep_crc32c.so).
 uint32_t Extend(uint32_t init_crc, const char* data, size_t n);
 
 // util/crc32c.h:20

@@ -13,6 +13,7 @@
 #include <condition_variable>
 #include <thread>
 #include <vector>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -232,13 +233,17 @@ int ensure_staging_once(HostStaging& s) {
 }
 
 // Pinned slots, device slots, streams and events of the host entry points, created on first use.  A failure
-// part-way frees what was created (nothing leaks into the next attempt) and is remembered, so the framing
-// writers' payload copies go straight to memcpy instead of retrying the allocation on every call.
+// part-way frees what was created (nothing leaks into the next attempt).  It is retried after a backoff that doubles
+// with each consecutive failure (10 ms .. 10 s): a transient shortage of pinned memory is not a permanent
+// KVSEP_ENOMEM for the context, and meanwhile the framing writers' payload copies go straight to memcpy instead of
+// retrying the allocation on every call.
 int ensure_staging(kvsep_crc32c_ctx* c) {
   HostStaging& s = ctx_staging(c);
   if (s.ready) return KVSEP_OK;
-  if (s.failed) {
-    set_last_error("host staging could not be allocated earlier on this context");
+  const int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                          std::chrono::steady_clock::now().time_since_epoch()).count();
+  if (s.failures && now < s.retry_at_ns) {
+    set_last_error("host staging could not be allocated on this context (retried after a backoff)");
     return KVSEP_ENOMEM;
   }
   DeviceGuard dg(ctx_device(c));
@@ -247,10 +252,13 @@ int ensure_staging(kvsep_crc32c_ctx* c) {
   if (rc != KVSEP_OK) {
     std::string msg = kvsep_last_error();
     release_staging(s);
-    s.failed = true;
+    const int64_t backoff = std::min<int64_t>(10'000'000ll << std::min<uint32_t>(s.failures, 10), 10'000'000'000ll);
+    ++s.failures;
+    s.retry_at_ns = now + backoff;
     set_last_error(msg.c_str());
     return rc;
   }
+  s.failures = 0;
   s.pool = copy_pool_create();
   s.ready = true;
   return KVSEP_OK;
@@ -586,9 +594,11 @@ void kvsep_host_free_pinned(void* p) {
   if (p) (void)hipHostFree(p);
 }
 
+int kvsep_abi_version(void) { return KVSEP_ABI_VERSION; }
+
 const char* kvsep_build_info(void) {
   return "kvsep_crc32c: gfx950 HIP kernels (LDS-replicated Z_1024 stride chains, v_perm addressing), "
-         "host SSE4.2 path, ABI 1";
+         "host SSE4.2 path, ABI 2";
 }
 
 }  // extern "C"

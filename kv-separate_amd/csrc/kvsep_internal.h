@@ -63,7 +63,10 @@ struct HostStaging {
   Scratch scratch[kSlots];
   CopyPool* pool = nullptr;
   bool ready = false;
-  bool failed = false;  // allocation failed once: not retried (ensure_staging)
+  // allocation failed: retried only after a backoff (ensure_staging), so a transient failure is not permanent and
+  // a persistent one does not cost an allocation attempt per call
+  int64_t retry_at_ns = 0;
+  uint32_t failures = 0;
 };
 
 void release_staging(HostStaging& s);

@@ -124,6 +124,7 @@ _SIGS = {
     "kvsep_host_free_pinned": (None, [ctypes.c_void_p]),
     "kvsep_last_error": (ctypes.c_char_p, []),
     "kvsep_build_info": (ctypes.c_char_p, []),
+    "kvsep_abi_version": (ctypes.c_int, []),
     "kvsep_device_count": (ctypes.c_int, []),
 }
 

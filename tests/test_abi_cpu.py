@@ -1,6 +1,7 @@
 """The C-ABI library loads and exports every symbol include/kvsep_crc32c.h declares, and its
 host-only legs (SSE4.2 Extend below the offload threshold, Mask/Unmask) are bit-exact.  No GPU."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -18,16 +19,35 @@ def test_library_exports_every_header_symbol():
     assert not missing, missing
 
 
+SHIM = os.path.join(os.path.dirname(kvsep.LIB_PATH), "libkvsep_leveldb_abi.so")
+
+
 def test_exports_leveldb_extend_cpp_symbol():
     """The link-level boundary: leveldb::crc32c::Extend(uint32_t, const char*, size_t) with C++ linkage
-    (util/crc32c.h:17), so a KVDB build keeps its own util/crc32c.h and only swaps util/crc32c.cc for the library."""
-    l = ctypes.CDLL(kvsep.LIB_PATH)
+    (util/crc32c.h:17), so a KVDB build keeps its own util/crc32c.h and only swaps util/crc32c.cc for the shim
+    libkvsep_leveldb_abi.so (over the engine library)."""
+    l = ctypes.CDLL(SHIM)
     f = getattr(l, "_ZN7leveldb6crc32c6ExtendEjPKcm")
     f.restype = ctypes.c_uint32
     f.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]
     assert f(0, b"123456789", 9) == 0xE3069283
     assert f(0, b"TestCRCBuffer", 13) == 0xDCBC59FA  # util/crc32c.cc:267-274 self-test
     assert f(0x12345678, None, 0) == 0x12345678
+
+
+def test_engine_library_does_not_export_the_leveldb_symbol():
+    """loading the engine (e.g. RTLD_GLOBAL next to a real LevelDB) must not interpose that LevelDB's
+    leveldb::crc32c::Extend -- the C++ symbol lives only in the drop-in shim."""
+    import subprocess
+    syms = subprocess.run(["nm", "-D", "--defined-only", kvsep.LIB_PATH], capture_output=True, text=True).stdout
+    assert "_ZN7leveldb6crc32c6ExtendEjPKcm" not in syms
+    shim = subprocess.run(["nm", "-D", "--defined-only", SHIM], capture_output=True, text=True).stdout
+    assert "_ZN7leveldb6crc32c6ExtendEjPKcm" in shim
+
+
+def test_abi_version():
+    assert kvsep.lib().kvsep_abi_version() == 2
+    assert "ABI 2" in kvsep.build_info()
 
 
 def test_no_environment_variable_reaches_the_kernel_choice():

@@ -1,5 +1,6 @@
 """The C++ drop-in header compiles against the reference's call pattern and passes
-util/crc32c_test.cc's assertions when linked to libkvsep_crc32c.so (host leg; no GPU needed)."""
+util/crc32c_test.cc's assertions when linked to libkvsep_leveldb_abi.so + libkvsep_crc32c.so (host leg; no GPU
+needed)."""
 import os
 import shutil
 import subprocess
@@ -17,7 +18,7 @@ def test_cpp_dropin(tmp_path):
     exe = tmp_path / "crc32c_dropin_test"
     subprocess.check_call(["g++", "-std=c++11", "-O2", "-I", os.path.join(ROOT, "include"),
                            os.path.join(ROOT, "tests", "cpp", "crc32c_dropin_test.cc"), "-L", libdir,
-                           "-lkvsep_crc32c", f"-Wl,-rpath,{libdir}", "-o", str(exe)])
+                           "-lkvsep_leveldb_abi", "-lkvsep_crc32c", f"-Wl,-rpath,{libdir}", "-o", str(exe)])
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "PASS" in r.stdout

@@ -102,6 +102,118 @@ def test_group_device_shards_vs_reference(group):
     assert (fb, nb) == (int(b[1]) + 100, 1)
 
 
+@pytest.fixture(scope="module")
+def group8():
+    # eight members: the 8-way byte-balanced partition, eight member host threads / staging
+    # pipelines / streams, and the first_bad / nbad reduction over eight parts -- on the one-GPU box as eight
+    # independent contexts on device 0
+    g = kvsep.Group([0] * 8)
+    yield g
+    g.close()
+
+
+def test_group8_vlog_scan_bad_record_in_last_member(group8):
+    """A config-5 vlog slice image (the reference's CRCs as the stored headers, db/value_log_writer.cc:57-60) scanned
+    by the 8-member group as GC / recovery scan a whole vlog (db/db_impl.cc:880-951 / :485-571), then with one bad
+    record inside the last member's range: the reader verdict (records kept, bytes dropped) is the reference reader's."""
+    n = 160
+    off, ln = W.cfg3_layout(vlog=True, count=n)
+    span = int(off[-1] + ln[-1])
+    img = splitmix64_bytes(span, W.SEED + 1, 0)
+    crc = np.fromfile(os.path.join(GOLDEN, "full_cfg5.u32"), dtype="<u4")[:n]
+    for i in range(n):
+        h = int(off[i]) - 8
+        img[h:h + 4] = np.frombuffer(kvsep.mask(int(crc[i])).to_bytes(4, "little"), np.uint8)
+        img[h + 4:h + 8] = np.frombuffer(int(ln[i]).to_bytes(4, "little"), np.uint8)
+    assert group8.size() == 8
+    assert group8.vlog_verify(img) == (n, n, span, 0)
+    b = kvsep.partition(ln, 8)
+    bad = int(b[7]) + 3  # inside member 7's part
+    assert bad < n
+    img[int(off[bad]) + 1000] ^= 0x01
+    assert group8.vlog_verify(img) == (n, bad, int(off[bad - 1] + ln[bad - 1]), int(ln[bad]))
+
+
+def test_group8_device_shards_index_base_vs_reference(group8):
+    """All of config 2 (the reference's whole-batch CRCs) as eight device shards with index_base: results, and the
+    global first_bad / nbad of stored words corrupted in members 2, 5 and 7."""
+    off, ln = W.cfg2_layout()
+    ref = np.fromfile(os.path.join(GOLDEN, "full_cfg2.u32"), dtype="<u4")
+    data = torch.empty(int(ln.sum()) + 64, dtype=torch.uint8, device=DEV)
+    kvsep.fill_splitmix64(data.data_ptr(), int(ln.sum()), W.SEED, 0)
+    b = kvsep.partition(ln, 8)
+    assert all(int(b[i + 1]) - int(b[i]) == 8192 for i in range(8))  # equal lengths: an exact byte split
+    shards, outs, exps = [], [], []
+    for i in range(8):
+        lo, hi = int(b[i]), int(b[i + 1])
+        o = torch.zeros(hi - lo, dtype=torch.int32, device=DEV)
+        outs.append(o)
+        shards.append({"base": data.data_ptr() + int(off[lo]), "off": u64(off[lo:hi] - off[lo]), "len": u64(ln[lo:hi]),
+                       "out": o, "total_bytes": int(ln[lo:hi].sum()), "max_len": 4096})
+        exps.append(np.array([kvsep.mask(int(c)) for c in ref[lo:hi]], np.uint32))
+    group8.batch_device(shards)
+    assert np.array_equal(np.concatenate([o.cpu().numpy().view(np.uint32) for o in outs]), ref)
+    ib = [int(b[i]) for i in range(8)]
+    d_exps = [torch.from_numpy(e.view(np.int32)).to(DEV) for e in exps]
+    assert group8.batch_device(shards, expected_masked=d_exps, index_base=ib) == (~0 & (2**64 - 1), 0)
+    for m, k in ((7, 8191), (5, 17), (2, 4000)):
+        exps[m][k] ^= 0x100
+    d_exps = [torch.from_numpy(e.view(np.int32)).to(DEV) for e in exps]
+    assert group8.batch_device(shards, expected_masked=d_exps, index_base=ib) == (ib[2] + 4000, 3)
+
+
+def test_group8_ragged_host_span_with_init_vs_oracle(group8, oracle):
+    """A ragged config-4-shaped host batch (Zipf lengths, capped so the test stays small) with per-block init words,
+    odd alignments: the 8-way partition by bytes, results and the verify reduction against the oracle."""
+    rng = np.random.default_rng(88)
+    ln = np.minimum(W.zipf_lengths(12000), 400_000).astype(np.uint64)
+    off = np.zeros(ln.size, np.uint64)
+    off[1:] = np.cumsum(ln[:-1] + np.uint64(5), dtype=np.uint64)
+    buf = splitmix64_bytes(int(off[-1] + ln[-1]) + 64, 8888, 0)
+    init = rng.integers(0, 2**32, ln.size, dtype=np.uint64).astype(np.uint32)
+    exp = oracle.batch(buf, off, ln, init, threads=8)
+    assert np.array_equal(group8.batch_host_span(buf, off, ln, init=init), exp)
+    b = kvsep.partition(ln, 8)
+    share = [int(ln[int(b[i]):int(b[i + 1])].sum()) for i in range(8)]
+    assert max(share) - min(share) <= 2 * int(ln.max())  # within a block or two of its byte share
+    stored = np.array([kvsep.mask(int(c)) for c in exp], np.uint32)
+    out, fb, nb = group8.batch_host_span(buf, off, ln, init=init, expected_masked=stored)
+    assert np.array_equal(out, exp) and (fb, nb) == (2**64 - 1, 0)
+    plant = [int(b[7]) + 1, int(b[3]) + 2, int(b[3]) + 3]
+    stored[plant] ^= 0x8
+    assert group8.batch_host_span(buf, off, ln, init=init, expected_masked=stored)[1:] == (min(plant), 3)
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (ADVICE r2: distinct-device group path)")
+def test_group_distinct_devices_vs_reference(oracle):
+    """The group over distinct devices: per-member DeviceGuard switching, scratch on each member's device, member
+    streams on different devices.  Runs only where two or more GPUs are visible (not on the one-GPU box)."""
+    ndev = min(torch.cuda.device_count(), 8)
+    g = kvsep.Group(list(range(ndev)))
+    try:
+        rng = np.random.default_rng(5)
+        ln = rng.integers(0, 200_000, 3000).astype(np.uint64)
+        off = np.zeros(ln.size, np.uint64)
+        off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+        buf = splitmix64_bytes(int(off[-1] + ln[-1]) + 64, 5150, 0)
+        exp = oracle.batch(buf, off, ln, None, threads=8)
+        assert np.array_equal(g.batch_host_span(buf, off, ln), exp)
+        b = kvsep.partition(ln, ndev)
+        shards, outs = [], []
+        for i in range(ndev):
+            lo, hi = int(b[i]), int(b[i + 1])
+            dv = torch.device("cuda", i)
+            d = torch.from_numpy(buf[int(off[lo]):int(off[hi - 1] + ln[hi - 1])].copy()).to(dv)
+            o = torch.zeros(hi - lo, dtype=torch.int32, device=dv)
+            outs.append(o)
+            shards.append({"base": d, "off": u64(off[lo:hi] - off[lo], dv), "len": u64(ln[lo:hi], dv), "out": o,
+                           "total_bytes": int(ln[lo:hi].sum()), "max_len": int(ln[lo:hi].max())})
+        g.batch_device(shards)
+        assert np.array_equal(np.concatenate([o.cpu().numpy().view(np.uint32) for o in outs]), exp)
+    finally:
+        g.close()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
