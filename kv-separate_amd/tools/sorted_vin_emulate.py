@@ -5,7 +5,7 @@ batch of tools/sorted_vin_probe.py (n = 70,000, lengths 0..39, correct stored wo
 If the emulator -- which runs the instructions exactly as the ISA defines them, every memory op complete before the next
 instruction -- reproduces the hardware's wrong CRCs for a variant, the generated code is wrong (a compiler/logic error
 one can trace here); if it computes them right while the hardware does not, the fault is in how the hardware executes
-that sequence (DESIGN.md §3.4).  CPU only; needs the .s from a --save-temps build of the KVSEP_DIAG device code.
+that sequence (DESIGN.md §3.5).  CPU only; needs the .s from a --save-temps build of the KVSEP_DIAG device code.
 usage: sorted_vin_emulate.py ASM [--variants 20,24,25,28] [--wg 0]"""
 import argparse
 import os

@@ -6,7 +6,7 @@ the .s hipcc writes with --save-temps -- instruction by instruction: 64-lane VGP
 scalar and vector memory, LDS and the cross-lane ops (ds_bpermute, DPP row shifts, readlane).  Every memory operation
 completes before the next instruction, so s_waitcnt is a no-op, and there is no notion of time: it answers "does this
 instruction sequence, executed as the ISA defines it, compute the right result?" -- separating a logic error in the
-generated code from a timing or hardware effect (DESIGN.md §3.4).
+generated code from a timing or hardware effect (DESIGN.md §3.5).
 
 Semantics follow the CDNA3/4 ISA for the opcodes listed in VALU / SALU / MEM below; anything else raises.
 """
@@ -142,7 +142,7 @@ class Wave:
     def __init__(self, wg, wave_id: int):
         self.wg = wg
         self.id = wave_id
-        self.v = np.zeros((512, 64), dtype=np.uint32)
+        self.v = np.zeros((512, 64), dtype=np.uint32)  # v509-v511: SDWA temporaries
         self.s = [0] * 128
         self.vcc = 0
         self.exec = M64
@@ -663,7 +663,56 @@ class Workgroup:
         raise EmuError('unknown ds op ' + k.text)
 
     # ------------------------------------------------------------------------------------------------------------
+    SDWA_TMP = (509, 510, 511)  # scratch VGPRs of the emulator (the kernels use at most 256)
+
+    def sdwa(self, w, k, op, o, act):
+        """VOP1/VOP2 SDWA: select bytes/words of the sources, run the plain op on temporaries, place the result per
+        dst_sel / dst_unused."""
+        if any(x.startswith('sext(') for x in o) or 'clamp' in k.mods:
+            raise EmuError('sdwa modifier ' + k.text)
+        t0, t1, td = self.SDWA_TMP
+        if op.startswith('v_cmp_'):  # VOPC SDWA: the destination is an SGPR pair / VCC
+            m = re.match(r'v_cmp_(\w+)_([ui])16_sdwa$', op)
+            if not m:
+                raise EmuError('sdwa compare ' + k.text)
+            for i, (t, sel) in enumerate(zip(o[1:3], (k.mods.get('src0_sel'), k.mods.get('src1_sel')))):
+                w.v[(t0, t1)[i]] = sdwa_sel(w.vget(t), sel) & np.uint32(0xFFFF)
+            plain = Insn(k.line, 'v_cmp_%s_%s32_e64 %s, v%d, v%d' % (m.group(1), m.group(2), o[0], t0, t1))
+            if m.group(2) == 'i':
+                for t in (t0, t1):
+                    w.v[t] = (w.v[t].astype(np.uint16).view(np.int16).astype(np.int32)).view(np.uint32)
+            return self.valu(w, plain, plain.op, plain.ops, act)
+        srcs = o[1:]
+        ops = ['v%d' % td]
+        for i, (t, sel) in enumerate(zip(srcs, (k.mods.get('src0_sel'), k.mods.get('src1_sel')))):
+            if t == 'vcc':
+                ops.append(t)
+                continue
+            w.v[(t0, t1)[i]] = sdwa_sel(w.vget(t), sel)
+            ops.append('v%d' % (t0, t1)[i])
+        plain = Insn(k.line, op[:-5] + ('_e64' if op[:-5].startswith('v_cmp') else '') + ' ' + ', '.join(ops))
+        self.valu(w, plain, plain.op, plain.ops, act)
+        r = w.v[td].copy()
+        dsel, unused = k.mods.get('dst_sel', 'DWORD'), k.mods.get('dst_unused', 'UNUSED_PAD')
+        if dsel != 'DWORD':
+            old = w.vget(o[0])
+            if dsel.startswith('BYTE_'):
+                sh, m = 8 * int(dsel[5:]), np.uint32(0xFF)
+            else:
+                sh, m = 16 * int(dsel[5:]), np.uint32(0xFFFF)
+            field = (r & m) << np.uint32(sh)
+            fmask = m << np.uint32(sh)
+            if unused == 'UNUSED_PRESERVE':
+                r = (old & ~fmask) | field
+            elif unused == 'UNUSED_PAD':
+                r = field
+            else:
+                raise EmuError('sdwa dst_unused ' + k.text)
+        w.vset(o[0], r)
+
     def valu(self, w, k, op, o, act):
+        if op.endswith('_sdwa'):
+            return self.sdwa(w, k, op, o, act)
         V = w.vget
         base = re.sub(r'_(e32|e64|sdwa|dpp)$', '', op)
         # compares
@@ -733,11 +782,6 @@ class Workgroup:
             return
         if base in ('v_and_b32', 'v_or_b32', 'v_xor_b32'):
             a, b = V(o[1]), V(o[2])
-            if op.endswith('_sdwa'):
-                a = sdwa_sel(a, k.mods.get('src0_sel'))
-                b = sdwa_sel(b, k.mods.get('src1_sel'))
-                if k.mods.get('dst_sel', 'DWORD') != 'DWORD':
-                    raise EmuError('sdwa dst ' + k.text)
             r = {'v_and_b32': a & b, 'v_or_b32': a | b, 'v_xor_b32': a ^ b}[base]
             w.vset(o[0], r)
             return
@@ -920,35 +964,90 @@ def pieces_kernarg(fields: dict, grid: int, threads: int) -> bytes:
     return bytes(ka)
 
 
+_FN_CACHE = {}
+
+
+def kernel_code(asm: str, name: str):
+    key = (asm, name, os.path.getmtime(asm))
+    if key not in _FN_CACHE:
+        _FN_CACHE[key] = load_function(asm, name)
+    return _FN_CACHE[key]
+
+
+def launch(mem: Memory, asm: str, name: str, threads: int, lds_bytes: int, fields: dict, grid: int, wgs=None) -> int:
+    """Run workgroups `wgs` (default: the whole grid, one after another) of a PiecesArgs kernel; returns the number of
+    wave-instructions executed.  Workgroups run to completion in order, so a dynamic (atomic-counter) schedule hands
+    every item to the first workgroup -- functionally the same result, a different interleaving."""
+    insns, labels = kernel_code(asm, name)
+    d_ka = mem.alloc(416, data=pieces_kernarg(fields, grid, threads))
+    steps = 0
+    for g in (range(grid) if wgs is None else wgs):
+        steps += Workgroup(mem, insns, labels, threads, lds_bytes, d_ka, g).run()
+    return steps
+
+
+SENTINEL = 0xDEADBEEF
+
+
+def batch_memory(data, off, ln, tabs: bytes, expect=None):
+    """Device image of one batch call: payload, descriptors, results (sentinel-filled), tables, verify words."""
+    n = int(np.asarray(off).size)
+    mem = Memory()
+    f = {"base": mem.alloc(data.size + 65536, data=data), "off": mem.alloc(8 * n, data=np.asarray(off, np.uint64)),
+         "len": mem.alloc(8 * n, data=np.asarray(ln, np.uint64)),
+         "out": mem.alloc(4 * n, data=np.full(n, SENTINEL, np.uint32)), "count": n, "piece_bytes": 128 * 1024,
+         "max_pieces": n, "static_contig": 1, "tabs": mem.alloc(len(tabs), data=tabs)}
+    if expect is not None:
+        f["expect"] = mem.alloc(4 * n, data=np.asarray(expect, np.uint32))
+        f["first_bad"] = mem.alloc(8, data=np.array([~np.uint64(0)], np.uint64))
+        f["nbad"] = mem.alloc(8)
+    return mem, f
+
+
+def batch_results(mem: Memory, f: dict):
+    """(out words, mask of blocks written, first_bad or -1, nbad)"""
+    out = mem.view(f["out"], 4 * f["count"]).view(np.uint32).copy()
+    fb = mem.r64(f["first_bad"]) if "first_bad" in f else (1 << 64) - 1
+    nb = mem.r64(f["nbad"]) if "nbad" in f else 0
+    # a written word equals the sentinel only by chance (1 in 2^32): callers compare against the oracle
+    return out, out != SENTINEL, (-1 if fb == (1 << 64) - 1 else fb), nb
+
+
 def run_batch_kernel(asm: str, name: str, threads: int, data: np.ndarray, off, ln, tabs: bytes, wg: int = 0,
                      grid: int = 256, hint: int = 0, expect=None, lds_bytes: int = 160768):
     """Run workgroup `wg` of a batch kernel (a PiecesArgs kernel in static, unplanned mode) over the given batch.
     Returns (out words, mask of blocks written, first_bad or -1, nbad, instructions executed)."""
-    n = int(np.asarray(off).size)
-    insns, labels = load_function(asm, name)
-    mem = Memory()
-    d_base = mem.alloc(data.size + 65536, data=data)
-    d_off = mem.alloc(8 * n, data=np.asarray(off, np.uint64))
-    d_len = mem.alloc(8 * n, data=np.asarray(ln, np.uint64))
-    sentinel = 0xDEADBEEF
-    d_out = mem.alloc(4 * n, data=np.full(n, sentinel, np.uint32))
-    d_tabs = mem.alloc(len(tabs), data=tabs)
-    f = {"base": d_base, "off": d_off, "len": d_len, "out": d_out, "count": n, "piece_bytes": 128 * 1024,
-         "max_pieces": n, "static_contig": 1, "hint": hint, "tabs": d_tabs}
-    d_fb = d_nb = None
-    if expect is not None:
-        f["expect"] = mem.alloc(4 * n, data=np.asarray(expect, np.uint32))
-        d_fb = f["first_bad"] = mem.alloc(8, data=np.array([~np.uint64(0)], np.uint64))
-        d_nb = f["nbad"] = mem.alloc(8)
-    d_ka = mem.alloc(416, data=pieces_kernarg(f, grid, threads))
-    w = Workgroup(mem, insns, labels, threads, lds_bytes, d_ka, wg)
-    steps = w.run()
-    out = mem.view(d_out, 4 * n).view(np.uint32).copy()
-    # a written word may equal the sentinel only by chance (1 in 2^32): the caller compares against the oracle
-    written = out != sentinel
-    fb = mem.r64(d_fb) if d_fb else (1 << 64) - 1
-    nb = mem.r64(d_nb) if d_nb else 0
-    return out, written, (-1 if fb == (1 << 64) - 1 else fb), nb, steps
+    mem, f = batch_memory(data, off, ln, tabs, expect)
+    f["hint"] = hint
+    steps = launch(mem, asm, name, threads, lds_bytes, f, grid, [wg])
+    return batch_results(mem, f) + (steps,)
+
+
+# DevTables field offsets (bytes), csrc/crc32c_device.hip
+TAB_ZSMALL = 4096 * 9 + 1024 + 4096   # z1024, z4, ztree[6], byte1, zpiece, znarrow -> zsmall[0]
+
+
+def run_planned_batch(asm: str, pieces: str, combine: str, data: np.ndarray, off, ln, tabs: bytes, piece_k: int = 0,
+                      grid: int = 256, expect=None):
+    """One planned (split-block) call as launch_batch_in issues it: the piece table built on the host exactly as
+    crc32c_plan_count_kernel / InclusiveSum / crc32c_plan_expand_kernel build it, the pieces kernel (dynamic
+    schedule; one workgroup takes every item), then every workgroup of the combine kernel.  Pieces are
+    zsmall[piece_k]'s 16 KiB << piece_k.  Returns (out, written, first_bad, nbad, instructions)."""
+    ln = np.asarray(ln, np.uint64)
+    n = ln.size
+    P = (16 * 1024) << piece_k
+    counts = np.where(ln < 2 * P, 1, ln // P).astype(np.uint64)
+    pstart = np.zeros(n + 1, np.uint64)
+    pstart[1:] = np.cumsum(counts, dtype=np.uint64)
+    npieces = int(pstart[-1])
+    pblk = np.repeat(np.arange(n, dtype=np.uint32), counts.astype(np.int64))
+    mem, f = batch_memory(data, off, ln, tabs, expect)
+    f.update(pstart=mem.alloc(8 * (n + 1), data=pstart), pblk=mem.alloc(4 * npieces, data=pblk),
+             partial=mem.alloc(4 * npieces), work_counter=mem.alloc(16), piece_bytes=P, max_pieces=npieces,
+             zpiece=f["tabs"] + TAB_ZSMALL + 4096 * piece_k, guided_div=0, guided_cap=0)
+    steps = launch(mem, asm, pieces, 512, 160768, f, grid, [0])
+    steps += launch(mem, asm, combine, 256, 4096, f, (n + 255) // 256)
+    return batch_results(mem, f) + (steps,)
 
 
 TABLES_DUMP = r'''

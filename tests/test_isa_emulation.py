@@ -1,4 +1,4 @@
-"""Functional emulation of the shipped narrow / sorted-window kernels' gfx950 assembly.  CPU only.
+"""Functional emulation of the shipped CRC kernels' gfx950 assembly.  CPU only.
 
 tools/wave_emu.py executes the compiled .s (the --save-temps output `make -C kv-separate_amd asm` keeps under build/)
 instruction by instruction -- 64-lane VGPRs under EXEC, SGPRs, LDS, scalar / vector memory, ds_bpermute and DPP --
@@ -6,7 +6,9 @@ for one workgroup of the real 256-workgroup grid, and the CRCs it writes are com
 sorted-window fault was a code-generation error of exactly this kind (a rematerialised table base restored under the
 narrowed EXEC of a nested divergent branch, so the slot-end lanes of every later group read the wrong table); the
 emulator reproduces it from the diag build's assembly (tools/sorted_vin_emulate.py) and this test runs the same check
-on every shipped narrow-family kernel, plain and verify forms, so a miscompile of that class fails on the CPU.
+on every shipped narrow-family kernel, plain and verify forms, so a miscompile of that class fails on the CPU.  The
+wide kernel runs too: unplanned (static runs, one workgroup of the grid) and planned (host-built piece table exactly
+as the plan kernels build it, the guided schedule, then every workgroup of the combine kernel).
 """
 import os
 import subprocess
@@ -78,3 +80,62 @@ def test_emulated_kernel_matches_oracle(env, label, tmpl, threads, kind):
     assert np.array_equal(np.nonzero(written_v)[0], mine)
     assert np.array_equal(out_v[mine], exp[mine])
     assert (fb, nb) == (int(plant.min()), 3)
+
+
+PIECES = "_ZN5kvsep20crc32c_pieces_kernelILb%dELb%dELi4ELb1ELb1ELi0ELi512ELb1ELb%dEEEvNS_10PiecesArgsE"
+COMBINE = "_ZN5kvsep21crc32c_combine_kernelILb%dEEEvNS_10PiecesArgsE"
+
+
+def _planted(exp, mask, idx):
+    stored = np.array([mask(int(x)) for x in exp], np.uint32)
+    stored[idx] ^= 0x100
+    return stored
+
+
+@pytest.mark.parametrize("verify", [0, 1])
+def test_emulated_wide_unplanned(env, verify):
+    """The wide kernel on an unsplit batch (static contiguous runs): one workgroup of the grid."""
+    E, tabs, mask, splitmix64_bytes = env
+    rng = np.random.default_rng(3)
+    n = 4096
+    ln = rng.integers(0, 5000, n).astype(np.uint64)
+    ln[rng.integers(0, n, 64)] = rng.integers(0, 16, 64)  # head/tail-only blocks
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(ln[:-1] + np.uint64(5), dtype=np.uint64)  # 5-B gaps: every start alignment
+    data = splitmix64_bytes(int(off[-1] + ln[-1]) + 4096, 13, 0)
+    exp = load_oracle().batch(data, off, ln, None, threads=8)
+    out, written, _, _, _ = E.run_batch_kernel(ASM, PIECES % (0, 0, 0), 512, data, off, ln, tabs, wg=7,
+                                               lds_bytes=160768)
+    mine = np.nonzero(written)[0]
+    assert mine.size > 0 and np.array_equal(out[mine], exp[mine])
+    if verify:
+        plant = mine[[0, mine.size - 1]]
+        out_v, wv, fb, nb, _ = E.run_batch_kernel(ASM, PIECES % (0, 0, 1), 512, data, off, ln, tabs, wg=7,
+                                                  expect=_planted(exp, mask, plant))
+        assert np.array_equal(np.nonzero(wv)[0], mine) and np.array_equal(out_v[mine], exp[mine])
+        assert (fb, nb) == (int(plant.min()), 2)
+
+
+@pytest.mark.parametrize("verify", [0, 1])
+def test_emulated_wide_planned_with_combine(env, verify):
+    """A split batch as the large configs run it: piece table, the wide kernel's guided schedule (one workgroup takes
+    every item here), the combine kernel's Horner step over the pieces; 16 KiB pieces, blocks up to 100 KiB."""
+    E, tabs, mask, splitmix64_bytes = env
+    rng = np.random.default_rng(4)
+    n = 40
+    ln = rng.integers(0, 100 * 1024, n).astype(np.uint64)
+    ln[:4] = [0, 1, 32 * 1024, 32 * 1024 - 1]  # empty, one byte, exactly 2P (split), just under 2P (not split)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(ln[:-1] + np.uint64(3), dtype=np.uint64)
+    data = splitmix64_bytes(int(off[-1] + ln[-1]) + 4096, 17, 0)
+    exp = load_oracle().batch(data, off, ln, None, threads=8)
+    expect = None
+    plant = np.array([2, 5, n - 1])  # a split block and two others
+    if verify:
+        expect = _planted(exp, mask, plant)
+    out, written, fb, nb, _ = E.run_planned_batch(ASM, PIECES % (1, 1, verify), COMBINE % verify, data, off, ln, tabs,
+                                                  expect=expect)
+    assert written.all()
+    assert np.array_equal(out, exp), f"{np.count_nonzero(out != exp)} wrong CRCs"
+    if verify:
+        assert (fb, nb) == (2, 3)
