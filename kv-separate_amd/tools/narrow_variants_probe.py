@@ -54,6 +54,24 @@ def parity(ctxs):
         bad = int((out.cpu().numpy().view(np.uint32) != exp).sum())
         print(f"parity n{v}: {bad} / {n} mismatches", flush=True)
         ok &= bad == 0
+    # many groups per wave (dynamic schedules grab most of them): 400 K blocks of 0..2000 B, hint 1024 (a third of the
+    # blocks over it: the deferred path) and the true hint
+    n = 400000
+    ln = rng.integers(0, 2001, n).astype(np.uint64)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(ln[:-1] + rng.integers(0, 3, n - 1).astype(np.uint64), dtype=np.uint64)
+    host = splitmix64_bytes(int(off[-1] + ln[-1]) + 256, 6, 0)
+    exp = oracle.batch(host, off, ln, None, threads=8)
+    d = torch.from_numpy(host).to(dev)
+    for v, ctx in ctxs.items():
+        for hint in (1024, 2000):
+            out = torch.zeros(n, dtype=torch.int32, device=dev)
+            for rep in range(3):  # back to back: each launch must leave the queue words as it found them
+                ctx.batch_device(d.data_ptr(), u64(off), u64(ln), out, max_len=hint, total_bytes=int(ln.sum()))
+            torch.cuda.synchronize()
+            bad = int((out.cpu().numpy().view(np.uint32) != exp).sum())
+            print(f"parity n{v} 400K hint {hint}: {bad} / {n} mismatches", flush=True)
+            ok &= bad == 0
     return ok
 
 
