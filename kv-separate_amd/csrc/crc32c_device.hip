@@ -82,8 +82,6 @@ struct PiecesArgs {
                                     // 0: adaptive, clamp(total / (64 * nwaves), 4, 32)
   uint32_t guided_cap;              // dynamic schedule: at most this many items per grab (0: no cap)
   uint64_t hint;                    // narrow kernel: the caller's max_len hint; longer blocks are deferred (exact)
-  uint32_t* nq;                     // dynamic narrow kernel: per-partition grab heads, arrivals, deferred lists
-                                    // (NarrowQueue layout; zero between launches: the last wave resets it)
   // verify form (kVerify kernels): Mask(crc of block b) must equal expect[b]; mismatches post the lowest block index
   // (atomicMin) and their number (atomicAdd) -- the check of db/value_log_reader.cc:109-122 / table/format.cc:99-106
   const uint32_t* expect;
@@ -458,15 +456,6 @@ __device__ __forceinline__ void verify_uniform(const PiecesArgs& a, uint32_t lan
   }
 }
 
-// Word layout of PiecesArgs::nq, the dynamic narrow kernel's queue (one 128-B line per counter): partition x's grab
-// head at [x * 32], its wave arrivals at [kNqDone + x * 32], its count of deferred groups at [kNqDefer + x * 32]; the
-// deferred-group bitmap (bit q & 31 of word q >> 5 for group q) from kNqList; from kNqList + groups on, each wave's
-// 64 junk words (the grab's lanes 1-63, see issue()).
-constexpr uint32_t kNqParts = 8;
-constexpr uint32_t kNqDone = kNqParts * 32;
-constexpr uint32_t kNqDefer = 2 * kNqParts * 32;
-constexpr uint32_t kNqList = 3 * kNqParts * 32;
-
 // A 32-bit global load (address space 1), for the stored words of the verify form.
 __device__ __forceinline__ uint32_t ld32(const uint32_t* p) {
   return *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(reinterpret_cast<uintptr_t>(p));
@@ -610,9 +599,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   const uint32_t tid = threadIdx.x;
-#ifdef KVSEP_STAMPS
-  unsigned long long e0, e1, r0, r1;
-  KVSEP_STAMP(e0);
+#ifdef KVSEP_STAMPS  // diagnostic build (tools/stamp_probe.hip): per-wave realtime (100 MHz) budget, see the end
+  unsigned long long r0, r1;
   KVSEP_RSTAMP(r0);
 #endif
   const uint32_t lane = tid & 63u;
@@ -752,27 +740,29 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   auto step = [&](uint64_t g, uint64_t end, Item& ia, Staged<kG>& A, Item& ib, Staged<kG>& B) {
     const bool hn = g + 1 < end;
 #ifdef KVSEP_STAMPS  // diagnostic build only (kv-separate_amd/tools/stamp_probe.hip)
-    unsigned long long t0, t1, t2, t3;
-    KVSEP_STAMP(t0);
+    unsigned long long t0;
+    KVSEP_RSTAMP(t0);
 #endif
     // The next item's HBM loads overlap the end of this item's compute (finish() stages them late, see
     // there).  The take is unconditional (the last item re-stages itself): on a path without it, this item's loads would be the most recent ones and the
     // compiler's counted wait (which merges both paths) would drain everything, vmcnt(0), on every item.
-#ifdef KVSEP_STAMPS
-    KVSEP_STAMP(t1);
-    KVSEP_STAMP(t2);
-#endif
     emit(ia, finish<kG, kNT, kAbl, kAlign>(lds, A, ia.reg0, lane, lc0, lc1, [&]() {
            if (kAhead) take(hn ? g + 1 : g, ib, B);
          }));
 #ifdef KVSEP_STAMPS
-    KVSEP_STAMP(t3);
-    if (lane == 0) {
-      unsigned long long* st = &g_kvsep_stamps[(uint64_t(blockIdx.x) * kWavesPerWg + wave) * 8];
-      st[0] += t1 - t0;
-      st[1] += t2 - t1;
-      st[2] += t3 - t2;
-      st[3] += 1;
+    {
+      // per wave: [0] / [1] ticks in whole-block items / in pieces of split blocks, [2] / [3] their counts, [7] the
+      // last item (bit 63 whole block, bit 62 a block's first piece, bits 40-61 its ticks, bits 0-39 its index)
+      unsigned long long t1;
+      KVSEP_RSTAMP(t1);
+      if (lane == 0) {
+        unsigned long long* st = &g_kvsep_stamps[(uint64_t(blockIdx.x) * kWavesPerWg + wave) * 8];
+        const unsigned long long d = t1 - t0;
+        st[ia.only ? 0 : 1] += d;
+        st[ia.only ? 2 : 3] += 1;
+        st[7] = (ia.only ? 1ull << 63 : 0ull) | (ia.reg0 != 0 ? 1ull << 62 : 0ull) | ((d & 0x3fffffull) << 40) |
+                (ia.g & 0xffffffffffull);
+      }
     }
 #endif
     if (!kAhead && hn) take(g + 1, ib, B);
@@ -784,7 +774,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   fill_lds<kThreads>(lds, &a.tabs->z1024[0][0], a.tabs, tid);
   __syncthreads();
 #ifdef KVSEP_STAMPS
-  KVSEP_STAMP(e1);
+  unsigned long long rf;
+  KVSEP_RSTAMP(rf);
 #endif
   while (grab()) {
     for (uint64_t ws = lo; ws < hi; ws += 64) {
@@ -798,15 +789,12 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
     }
   }
 #ifdef KVSEP_STAMPS
-  unsigned long long e2;
-  KVSEP_STAMP(e2);
   KVSEP_RSTAMP(r1);
-  if (lane == 0) {  // [4] LDS fill cycles, [5] work-loop cycles, [6] realtime ticks (100 MHz), [7] entry cycle
+  if (lane == 0) {  // [4] entry, [5] LDS fill done, [6] exit (realtime)
     unsigned long long* st = &g_kvsep_stamps[(uint64_t(blockIdx.x) * kWavesPerWg + wave) * 8];
-    st[4] = e1 - e0;
-    st[5] = e2 - e1;
-    st[6] = r1 - r0;
-    st[7] = r0;
+    st[4] = r0;
+    st[5] = rf;
+    st[6] = r1;
   }
 #endif
 }
@@ -1077,19 +1065,8 @@ __device__ __forceinline__ void narrow_deferred(const PiecesArgs& a, const uint8
 // workgroups than fit at once is the same computation (the hardware dispatcher then hands out the runs).
 // kVerify: the verify form (verify_wave after each group; the stored words are loaded just before the next group's
 // staging).
-//
-// kDyn: a dynamic schedule instead of the static runs.  The groups are cut into 8 contiguous partitions, one per
-// residue of blockIdx mod 8 (the hardware deals workgroups to the 8 XCDs round-robin, so a partition is normally one
-// XCD's; nothing depends on it); each wave takes one group of its partition statically, then grabs the partition's
-// next group from the partition's head word (one returning atomic per group, issued a group ahead of its descriptor
-// load, so its latency hides under the current group).  Waves whose workgroup started late or whose loads the memory
-// system serves later take fewer groups.  Blocks over the hint cannot be redone from a run at the end: a group with
-// one is appended to the partition's deferred list, and the partition's last wave to finish redoes the listed groups'
-// long blocks (narrow_deferred) and then zeroes the partition's words for the next launch (stream order: nothing else
-// runs on them in between).  Every counter and list word is read and written only by atomics (memory-side, coherent
-// across XCDs).
 template <int kG, bool kNT, int kThreads, bool kOverlap = false, int kAbl = 0, bool kAlignN = true,
-          typename Lay = LdsFull, bool kVerify = false, int kDyn = 0>
+          typename Lay = LdsFull, bool kVerify = false>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   __shared__ __attribute__((aligned(16))) uint8_t lds[Lay::kBytes];
@@ -1107,79 +1084,10 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   // contiguous run of whole groups per wave.  Runs are numbered wave-major (run w*grid + b), so when there are
   // fewer groups than waves the busy waves are spread over every CU instead of filling the first CUs.
   const uint64_t groups = (a.count + kPerGroup - 1) / kPerGroup;
-  uint64_t lo, hi;
-  // kDyn: this wave's partition [plo, phi) (groups), its wave count wx, and its queue words
-  uint64_t plo = 0, phi = 0;
-  uint32_t wx = 0, wgp = 0;  // waves and workgroups of the partition
-  __shared__ uint32_t wg_arrivals;  // kDyn: waves of this workgroup done (zeroed before the fill's barrier)
-  uint32_t *qhead = nullptr, *qdone = nullptr, *qdefer = nullptr, *qbits = nullptr, *qjunk = nullptr;
-  uint64_t qs = 0, qe = 0;  // kDyn 2/3 (diag): the static run [qs, qe) walked through the dynamic kernel's machinery
-  if constexpr (kDyn != 0) {
-    const uint32_t np = kDyn != 2 && kDyn != 3 && (gridDim.x % kNqParts) == 0 ? kNqParts : 1u;
-    const uint32_t part = blockIdx.x % np, wgs = gridDim.x / np, wgi = blockIdx.x / np;
-    wx = wgs * kWavesPerWg;
-    wgp = wgs;
-    plo = groups * part / np;
-    phi = groups * (part + 1) / np;
-    qhead = a.nq + part * 32u;
-    qdone = a.nq + kNqDone + part * 32u;
-    qdefer = a.nq + kNqDefer + part * 32u;
-    qbits = a.nq + kNqList;
-    qjunk = a.nq + kNqList + groups + (uint64_t(blockIdx.x) * kWavesPerWg + wave) * 64u;
-    uint64_t q0 = plo + uint64_t(wave) * wgs + wgi;  // the static first group (wave-major)
-    if constexpr (kDyn >= 2 && kDyn <= 4) {  // diag: the static kernel's run (4: grabs on the partition heads too)
-      const uint64_t gper = (groups + nwaves - 1) / nwaves;
-      qs = (uint64_t(wave) * gridDim.x + blockIdx.x) * gper;
-      qe = qs + gper < groups ? qs + gper : groups;
-      q0 = qs < qe ? qs : (kDyn == 4 ? groups : phi);
-      if (kDyn == 4) {
-        plo = 0;
-        phi = groups;
-      }
-    }
-    if constexpr (kDyn == 5) qs = q0;  // diag: round-robin over the partition, the order a balanced grab gives
-    lo = q0 < phi ? q0 * kPerGroup : a.count;
-    hi = a.count;  // block bound of every group (loads clamp to it); groups past phi are `a.count`: empty
-  } else {
-    const uint64_t gper = (groups + nwaves - 1) / nwaves;
-    lo = (uint64_t(wave) * gridDim.x + blockIdx.x) * gper * kPerGroup;
-    hi = lo + gper * kPerGroup;
-    if (hi > a.count) hi = a.count;
-  }
-  // kDyn: the pending grab (lane 0's atomic return) and the group after the next one (a block index; a.count = none)
-  uint32_t tgrab = 0;
-  uint64_t gnx = a.count;
-  bool marked = false;  // kDyn, wave-uniform: this wave marked a deferred group
-  // A grab is one atomic instruction in full EXEC, issued on every path: lane 0 increments the head, lanes 1-63 this
-  // wave's own junk words.  A grab inside `if (lane == 0)` leaves a path without it (the EXEC-zero skip), and the
-  // compiler's wait for its result then drains every staged row load (s_waitcnt vmcnt(0) per group); an atomicAdd
-  // is also rewritten by the AMDGPU atomic optimizer into a form that reads the result at once.  atomicInc (wraps
-  // at 2^32 - 1, never reached) is left alone.
-  auto issue = [&]() {
-    if constexpr (kDyn == 6) {  // diag: the grab in lane 0 only (a divergent branch), no junk lanes
-      uint32_t v = 0;
-      if (lane == 0) v = atomicInc(qhead, 0xffffffffu);
-      tgrab = v;
-    } else if constexpr (kDyn != 3 && kDyn != 5) {
-      tgrab = atomicInc(lane ? qjunk + lane : qhead, 0xffffffffu);
-    }
-  };
-  // The grab's value is read (sgrab) at the next take, right after that take's staging loads: the take has waited for
-  // its descriptors, which went out after the grab, so no wait of its own lands on the staged rows.  Read at the end of
-  // the step instead, the compiler's wait for it also took the next group's first staged loads (-25 % on 4 KiB blocks).
-  uint32_t sgrab = 0;
-  auto resolve = [&]() -> uint64_t {
-    if constexpr (kDyn >= 2 && kDyn <= 4) {
-      ++qs;
-      return qs < qe ? qs * kPerGroup : a.count;
-    }
-    if constexpr (kDyn == 5) {
-      qs += wx;
-      return qs < phi ? qs * kPerGroup : a.count;
-    }
-    const uint64_t q = plo + wx + sgrab;
-    return q < phi ? q * kPerGroup : a.count;
-  };
+  const uint64_t gper = (groups + nwaves - 1) / nwaves;
+  const uint64_t lo = (uint64_t(wave) * gridDim.x + blockIdx.x) * gper * kPerGroup;
+  uint64_t hi = lo + gper * kPerGroup;
+  if (hi > a.count) hi = a.count;
 
   // Descriptors run one group ahead of the staging: taking group g stages its rows from descriptors loaded
   // when group g-8 was taken, then loads those of group g+8 (each lane its slot's block: one 64-B line per
@@ -1217,9 +1125,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   const uint32_t hint32 = uint32_t(a.hint);  // <= 64 KiB (use_narrow)
   auto take = [&](uint64_t g, NItem& it, NStaged<kG>& st) {
     const bool in = g + slot < hi;
-    // kDyn: branch-free, so the wait for the descriptors (and with them the grab issued just before them) is on every
-    // path; the grab is read out right after the staging loads (sgrab)
-    const bool over = kDyn ? in & ((dn.lenhi != 0) | (dn.len > hint32)) : in && (dn.lenhi != 0 || dn.len > hint32);
+    const bool over = in && (dn.lenhi != 0 || dn.len > hint32);
     deferred |= __builtin_amdgcn_ballot_w64(over) != 0;
     const bool live = in && !over;
     const uintptr_t ps = live ? reinterpret_cast<uintptr_t>(a.base) + dn.off : dummy;
@@ -1235,10 +1141,9 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     }
     it.kmax = km;
     it.kmin = kn;
-    if constexpr (kDyn) sgrab = uint32_t(__builtin_amdgcn_readlane(int(tgrab), 0));
   };
   auto step = [&](uint64_t g, NItem& ia, NStaged<kG>& A, NItem& ib, NStaged<kG>& B) {
-    const uint64_t gn = kDyn ? gnx : g + kPerGroup;
+    const uint64_t gn = g + kPerGroup;
     // the next group is staged inside nfinish, after this group's last row loads; unconditional (past the
     // end it is an empty group of dummy loads: see the wide kernel's step())
     // the verify form: this group's stored words (uniform base + a clamped 32-bit lane offset), issued before the
@@ -1257,28 +1162,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     // cover when skipped) would make that wait one count short and hold up the next group's first staged load
     if (kVerify) verify_wave(a, lane, mine, g, slot, ~reg, ex);
     if (mine) emit_block(a, g + slot, ~reg);
-    if constexpr (kDyn) {
-      // wave-uniform, rare: the group is marked in the deferred bitmap.  No-return atomics: a returned value used
-      // here would be waited for with every staged row load behind it (vmcnt(0))
-      if (__builtin_amdgcn_ballot_w64(ia.over)) {
-        const uint32_t q = uint32_t(g / kPerGroup);
-        if (lane == 0) {
-          atomicOr(qbits + (q >> 5), 1u << (q & 31u));
-          atomicAdd(qdefer, 1u);
-        }
-        marked = true;
-      }
-      // the group after the next: the grab issued a group ago, the next grab, then the descriptors.  The grab goes out
-      // BEFORE the descriptor loads: the next take's wait for those descriptors then covers it too, so reading it a
-      // group later needs no wait of its own (every step resolves one grab and issues one; past the partition's end
-      // they only count up)
-      const uint64_t g2 = resolve();
-      issue();
-      load_desc(g2, dn);
-      gnx = g2;
-    } else {
-      load_desc(gn + kPerGroup, dn);  // here, where this group's registers are dead
-    }
+    load_desc(gn + kPerGroup, dn);  // here, where this group's registers are dead
     return gn < hi;
   };
 
@@ -1301,40 +1185,26 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
 #endif
   // The first group's descriptors are fetched during the LDS fill.  Staging its rows before the fill as well
   // measured 4-7 % slower on 256 MiB-1 GiB batches of 4 KiB blocks: the fill then waits behind them.
-  // kDyn: the second group's descriptors come from the first grab, issued before the fill
-  auto second = [&]() {
-    if constexpr (kDyn) {
-      gnx = resolve();
-      issue();
-      load_desc(gnx, dn);
-    } else {
-      load_desc(lo + kPerGroup, dn);
-    }
-  };
   if (kOverlap) {
     // descriptors, then the table loads, then the first group's rows: the LDS stores wait for the tables
     // only, so the first HBM round trip overlaps the fill.  Unconditional (an idle wave stages an empty
     // group), so the store's wait count is the same on every path.
     load_desc(lo, dn);
-    if (kDyn) issue();  // every wave grabs once up front (an idle one too: the grab is on every path)
     auto mid = [&]() {
       take(lo, cur, S);
-      second();
+      load_desc(lo + kPerGroup, dn);
     };
     if constexpr (Lay::kCompact) fill_lds_compact<kThreads>(lds, &a.tabs->znarrow[0][0], a.tabs, tid, mid);
     else fill_lds<kThreads, true>(lds, &a.tabs->znarrow[0][0], a.tabs, tid, mid);
-    if (kDyn && tid == 0) wg_arrivals = 0;
     __syncthreads();
   } else {
     if (lo < hi) load_desc(lo, dn);
-    if (kDyn) issue();  // every wave grabs once up front (an idle one too: the grab is on every path)
     if constexpr (Lay::kCompact) fill_lds_compact<kThreads>(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
     else fill_lds<kThreads, true>(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
-    if (kDyn && tid == 0) wg_arrivals = 0;
     __syncthreads();
     if (lo < hi) {
       take(lo, cur, S);
-      second();
+      load_desc(lo + kPerGroup, dn);
     }
   }
   KVSEP_NSTAMP(1);
@@ -1343,22 +1213,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
 #else
 #define KVSEP_NSTEP() do {} while (0)
 #endif
-  if constexpr (kDyn) {
-    if (lo < hi) {
-      for (uint64_t g = lo;;) {  // each step takes its next group from gnx (the grab chain)
-        uint64_t gn = gnx;
-        const bool more = step(g, cur, S, nxt, T);
-        KVSEP_NSTEP();
-        if (!more) break;
-        g = gn;
-        gn = gnx;
-        const bool more2 = step(g, nxt, T, cur, S);
-        KVSEP_NSTEP();
-        if (!more2) break;
-        g = gn;
-      }
-    }
-  } else if (lo < hi) {
+  if (lo < hi) {
     for (uint64_t g = lo;; g += 2 * kPerGroup) {
       const bool more = step(g, cur, S, nxt, T);
       KVSEP_NSTEP();
@@ -1371,57 +1226,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   KVSEP_NSTAMP(7);
 #undef KVSEP_NSTEP
 #undef KVSEP_NSTAMP
-  if constexpr (kDyn) {
-    // Arrival: every grab and list append of this wave has returned (performed) before its arrival is counted, so
-    // the last wave to arrive sees the whole list and no grab can follow its reset.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (marked) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // its bitmap marks before its arrival
-    uint32_t ln0;  // the lane index again (a value kept live across the work loop costs a VGPR at the cap)
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln0));
-    // arrivals counted per workgroup in LDS first: a global word taking all 512 waves of a partition serialises them
-    // at the end of the kernel (one returning atomic per wave on one word: ~6 us on 4 KiB-block batches)
-    uint32_t la = 0;
-    if (ln0 == 0) la = atomicAdd(&wg_arrivals, 1u);
-    if (uint32_t(__builtin_amdgcn_readlane(int(la), 0)) != kWavesPerWg - 1) return;
-    uint32_t d = 0;
-    if (ln0 == 0) d = atomicAdd(qdone, 1u);
-    if (uint32_t(__builtin_amdgcn_readlane(int(d), 0)) == wgp - 1) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      uint32_t nd = 0;
-      if (ln0 == 0) nd = atomicAdd(qdefer, 0u);
-      if (__builtin_amdgcn_readlane(int(nd), 0) != 0) {
-        // the partition's marked groups: each bitmap word taken and cleared (only this partition's bits: the edge
-        // words are shared with the neighbours) by one atomicAnd, 64 words per instruction
-        const uint64_t wlast = (phi - 1) >> 5;
-        for (uint64_t w0 = plo >> 5; w0 <= wlast; w0 += 64) {
-          const uint64_t w = w0 + ln0;
-          uint32_t bits = 0;
-          if (w <= wlast) {
-            const uint64_t q0 = w << 5;
-            const uint32_t lo_b = plo > q0 ? uint32_t(plo - q0) : 0u;
-            const uint32_t hi_b = phi < q0 + 32 ? uint32_t(phi - q0) : 32u;
-            const uint32_t own = (hi_b >= 32 ? ~0u : ((1u << hi_b) - 1u)) & ~((1u << lo_b) - 1u);
-            bits = atomicAnd(qbits + w, ~own) & own;
-          }
-          for (uint64_t any = __builtin_amdgcn_ballot_w64(bits != 0); any; any &= any - 1) {
-            const uint32_t k = uint32_t(__builtin_ctzll(any));
-            for (uint32_t bw = uint32_t(__builtin_amdgcn_readlane(int(bits), int(k))); bw; bw &= bw - 1) {
-              const uint64_t g0 = ((w0 + k) * 32u + uint32_t(__builtin_ctz(bw))) * kPerGroup;
-              narrow_deferred<kG, kNT, kAlignN, Lay, kVerify>(a, lds, g0,
-                                                              g0 + kPerGroup < a.count ? g0 + kPerGroup : a.count, dummy);
-            }
-          }
-        }
-      }
-      if (ln0 == 0) {
-        atomicExch(qhead, 0u);
-        atomicExch(qdefer, 0u);
-        atomicExch(qdone, 0u);
-      }
-    }
-  } else if (deferred) {
-    narrow_deferred<kG, kNT, kAlignN, Lay, kVerify>(a, lds, lo, hi, dummy);
-  }
+  if (deferred) narrow_deferred<kG, kNT, kAlignN, Lay, kVerify>(a, lds, lo, hi, dummy);
 }
 
 // Bitonic sort of one (key, idx) pair per lane over the wavefront, ascending by key (ties by idx, so the two
@@ -1925,24 +1730,6 @@ int release(Scratch& sc, hipStream_t s) {
   return KVSEP_OK;
 }
 
-// The dynamic narrow kernel's queue: kNqList counter words, one list word per 8-block group, then 64 junk words per
-// wave of the grid (`waves`).  Zeroed here once; every launch leaves the counters zero again (its partitions' last
-// waves reset their words).
-int ensure_nq(Scratch& sc, uint64_t groups, uint64_t waves) {
-  const uint64_t words = kNqList + groups + waves * 64;
-  if (sc.d_nq && words <= sc.cap_nq_words) return KVSEP_OK;
-  int rc = quiesce(sc);
-  if (rc) return rc;
-  hipFree(sc.d_nq);
-  sc.d_nq = nullptr;
-  sc.cap_nq_words = 0;
-  const uint64_t w = std::max<uint64_t>(words, kNqList + (1 << 14) + waves * 64);
-  KVSEP_HIP(hipMalloc(&sc.d_nq, w * 4));
-  KVSEP_HIP(hipMemset(sc.d_nq, 0, w * 4));
-  sc.cap_nq_words = w;
-  return KVSEP_OK;
-}
-
 // SST verify scratch (len + 1 and the stored trailer words per block).
 int ensure_sst(Scratch& sc, uint64_t count) {
   if (count <= sc.cap_sst) return KVSEP_OK;
@@ -2290,29 +2077,6 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
       case 40: crc32c_narrow_kernel<16, true, 256><<<grid, 256, 0, s>>>(a); break;
       case 41: crc32c_narrow_kernel<8, true, 256><<<grid, 256, 0, s>>>(a); break;
       case 42: crc32c_narrow_kernel<16, true, 256, true><<<grid, 256, 0, s>>>(a); break;
-      // dynamic schedule (per-partition grab heads): 43: 16-wave workgroups; 44: 8-wave, fill overlapped
-      // 45 / 46: the static runs walked through the dynamic kernel's machinery, with (one head) / without the grab
-      // atomics; 47: static runs with grabs on the 8 partition heads (results unused); 48: round-robin over each
-      // partition (a perfectly balanced grab order) without atomics; 49: 43 with the grab in lane 0 only
-      case 43:
-      case 44:
-      case 45:
-      case 46:
-      case 47:
-      case 48:
-      case 49: {
-        int rc = ensure_nq(sc, (count + 7) / 8, uint64_t(grid) * (nv == 44 ? 8 : 16));
-        if (rc) return rc;
-        a.nq = sc.d_nq;
-        if (nv == 43) crc32c_narrow_kernel<4, true, 1024, false, 0, true, LdsFull, false, 1><<<grid, 1024, 0, s>>>(a);
-        else if (nv == 44) crc32c_narrow_kernel<4, true, 512, true, 0, true, LdsFull, false, 1><<<grid, 512, 0, s>>>(a);
-        else if (nv == 45) crc32c_narrow_kernel<4, true, 1024, false, 0, true, LdsFull, false, 2><<<grid, 1024, 0, s>>>(a);
-        else if (nv == 46) crc32c_narrow_kernel<4, true, 1024, false, 0, true, LdsFull, false, 3><<<grid, 1024, 0, s>>>(a);
-        else if (nv == 47) crc32c_narrow_kernel<4, true, 1024, false, 0, true, LdsFull, false, 4><<<grid, 1024, 0, s>>>(a);
-        else if (nv == 48) crc32c_narrow_kernel<4, true, 1024, false, 0, true, LdsFull, false, 5><<<grid, 1024, 0, s>>>(a);
-        else crc32c_narrow_kernel<4, true, 1024, false, 0, true, LdsFull, false, 6><<<grid, 1024, 0, s>>>(a);
-        break;
-      }
 #endif
       case 9: crc32c_narrow_kernel<4, true, 512, true><<<grid, 512, 0, s>>>(a); break;
       case 20: crc32c_narrow_sorted_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
@@ -2352,7 +2116,6 @@ void free_scratch(Scratch& sc) {
   if (sc.used && sc.last_use) (void)hipEventSynchronize(sc.last_use);
   free_plan(sc);
   hipFree(sc.d_counter);
-  hipFree(sc.d_nq);
   hipFree(sc.d_verify);
   hipFree(sc.d_sst_len1);
   hipFree(sc.d_sst_stored);

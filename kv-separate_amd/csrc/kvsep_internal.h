@@ -23,8 +23,6 @@ struct Scratch {
   void* d_scan_tmp = nullptr;
   size_t scan_tmp_bytes = 0;
   uint32_t* d_counter = nullptr;
-  uint32_t* d_nq = nullptr;  // the dynamic narrow kernel's queue words (zeroed once; each launch leaves them zero)
-  uint64_t cap_nq_words = 0;
   unsigned long long* d_verify = nullptr;  // [first_bad, nbad] when the caller passes none
   uint64_t* d_sst_len1 = nullptr;           // SST verify: len + 1 ...
   uint32_t* d_sst_stored = nullptr;         // ... and the stored trailer words

@@ -1,7 +1,10 @@
-// stamp_probe.hip -- DIAGNOSTIC build of the CRC kernel with s_memtime stamps around the work-loop
-// segments (cdna_hip_programming.md §7 "In-kernel stamps"); never used for timing numbers, only for the
-// SHARES of a wave's time per item.  Build: hipcc --offload-arch=gfx950 -O3 -o stamp_probe stamp_probe.hip
-// Usage: stamp_probe <block_len> <count>
+// stamp_probe.hip -- DIAGNOSTIC build of the wide CRC kernel with s_memrealtime stamps (100 MHz) per wave: entry,
+// LDS fill done, exit, the ticks spent in whole-block items and in pieces of split blocks, and the last item of the
+// wave (crc32c_pieces_kernel's KVSEP_STAMPS block).  Never used for timing numbers, only for a per-wave time budget.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o stamp_probe stamp_probe.hip
+// Usage: stamp_probe <layout.bin> <stamps_out.bin> [reps]
+//   layout.bin: u64 count, then off[count], len[count] (tools/wstamp_analyze.py writes it); the span is filled with
+//   the splitmix64 stream on the device.  stamps_out.bin: the 8192 x 8 u64 stamp words of the last rep.
 #define KVSEP_STAMPS 1
 #include "../csrc/crc32c_device.hip"
 #include "../csrc/crc32c_host.cpp"
@@ -10,46 +13,53 @@
 #include <vector>
 
 int main(int argc, char** argv) {
-  const uint64_t blen = argc > 1 ? strtoull(argv[1], nullptr, 0) : 4096;
-  const uint64_t count = argc > 2 ? strtoull(argv[2], nullptr, 0) : 65536;
+  if (argc < 3) {
+    printf("usage: stamp_probe <layout.bin> <stamps_out.bin> [reps]\n");
+    return 2;
+  }
+  const int reps = argc > 3 ? atoi(argv[3]) : 3;
+  FILE* f = fopen(argv[1], "rb");
+  if (!f) { printf("cannot open %s\n", argv[1]); return 1; }
+  uint64_t count = 0;
+  if (fread(&count, 8, 1, f) != 1) return 1;
+  std::vector<uint64_t> off(count), len(count);
+  if (fread(off.data(), 8, count, f) != count || fread(len.data(), 8, count, f) != count) return 1;
+  fclose(f);
+  uint64_t span = 0, total = 0, maxlen = 0;
+  for (uint64_t i = 0; i < count; ++i) {
+    span = std::max(span, off[i] + len[i]);
+    total += len[i];
+    maxlen = std::max(maxlen, len[i]);
+  }
   kvsep_crc32c_ctx* ctx = nullptr;
   if (kvsep_crc32c_ctx_create(0, &ctx)) { printf("ctx: %s\n", kvsep_last_error()); return 1; }
   uint8_t* data; uint64_t *doff, *dlen; uint32_t* out;
-  hipMalloc(&data, blen * count + 64);
-  kvsep_fill_splitmix64_device(nullptr, data, blen * count, 1, 0);
-  std::vector<uint64_t> off(count), len(count, blen);
-  for (uint64_t i = 0; i < count; ++i) off[i] = i * blen;
+  if (hipMalloc(&data, span + 64) != hipSuccess) { printf("hipMalloc %lu failed\n", (unsigned long)span); return 1; }
+  kvsep_fill_splitmix64_device(nullptr, data, span, 1, 0);
   hipMalloc(&doff, count * 8); hipMalloc(&dlen, count * 8); hipMalloc(&out, count * 4);
   hipMemcpy(doff, off.data(), count * 8, hipMemcpyHostToDevice);
   hipMemcpy(dlen, len.data(), count * 8, hipMemcpyHostToDevice);
-  for (int rep = 0; rep < 3; ++rep) {
-    std::vector<unsigned long long> z(8192 * 8, 0);
+  std::vector<unsigned long long> z(8192 * 8, 0);
+  for (int rep = 0; rep < reps; ++rep) {
+    std::fill(z.begin(), z.end(), 0ull);
     hipMemcpyToSymbol(HIP_SYMBOL(kvsep::g_kvsep_stamps), z.data(), z.size() * 8);
     hipEvent_t ev0, ev1;
     hipEventCreate(&ev0); hipEventCreate(&ev1);
     hipEventRecord(ev0, nullptr);
-    kvsep_crc32c_batch_device(ctx, nullptr, data, doff, dlen, nullptr, out, count, blen * count, blen);
+    const int rc = kvsep_crc32c_batch_device(ctx, nullptr, data, doff, dlen, nullptr, out, count, total, maxlen);
     hipEventRecord(ev1, nullptr);
     hipDeviceSynchronize();
+    if (rc) { printf("batch: %s\n", kvsep_last_error()); return 1; }
     float ms = 0;
     hipEventElapsedTime(&ms, ev0, ev1);
-    hipMemcpyFromSymbol(z.data(), HIP_SYMBOL(kvsep::g_kvsep_stamps), z.size() * 8);
-    double s[3] = {0, 0, 0}, n = 0;
-    double fill = 0, loop = 0, rt = 0, nw = 0;
-    unsigned long long rmin = ~0ull, rmax = 0;
-    for (int w = 0; w < 8192; ++w) {
-      for (int k = 0; k < 3; ++k) s[k] += z[w * 8 + k];
-      n += z[w * 8 + 3];
-      if (z[w * 8 + 7]) {
-        fill += z[w * 8 + 4]; loop += z[w * 8 + 5]; rt += z[w * 8 + 6]; nw += 1;
-        rmin = std::min(rmin, z[w * 8 + 7]); rmax = std::max(rmax, z[w * 8 + 7] + z[w * 8 + 6]);
-      }
-    }
-    printf("  event %.1f us | waves %.0f: mean fill %.0f cyc, loop %.0f cyc, wave span %.1f us (realtime), "
-           "clock %.2f GHz | first entry -> last exit %.1f us\n", ms * 1e3, nw, fill / nw, loop / nw,
-           rt / nw / 100.0, (fill + loop) / (rt / 100.0) / 1e3 / 1.0, (rmax - rmin) / 100.0);
-    printf("len %lu count %lu: per item cycles  take-next %.0f  wait-data %.0f  compute %.0f  (items %.0f)\n",
-           (unsigned long)blen, (unsigned long)count, s[0] / n, s[1] / n, s[2] / n, n);
+    printf("rep %d: %.3f ms (%.1f GB/s over %lu blocks, %lu B)\n", rep, ms, total / (ms * 1e6), (unsigned long)count,
+           (unsigned long)total);
+    fflush(stdout);
   }
+  hipMemcpyFromSymbol(z.data(), HIP_SYMBOL(kvsep::g_kvsep_stamps), z.size() * 8);
+  FILE* o = fopen(argv[2], "wb");
+  if (!o) return 1;
+  fwrite(z.data(), 8, z.size(), o);
+  fclose(o);
   return 0;
 }

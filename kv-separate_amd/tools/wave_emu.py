@@ -945,24 +945,22 @@ class Workgroup:
 
 
 # ------------------------------------------------------------------------------------------------------------------
-# PiecesArgs (csrc/crc32c_device.hip) field offsets; the hidden arguments follow the 168-byte struct
+# PiecesArgs (csrc/crc32c_device.hip) field offsets; the hidden arguments follow the 160-byte struct
 PIECES_ARGS = {"base": 0, "off": 8, "len": 16, "init": 24, "out": 32, "count": 40, "pstart": 48, "pblk": 56,
                "partial": 64, "work_counter": 72, "piece_bytes": 80, "zpiece": 88, "max_pieces": 96,
                "static_contig": (104, "<I"), "guided_div": (108, "<I"), "guided_cap": (112, "<I"), "hint": 120,
-               "nq": 128, "expect": 136, "first_bad": 144, "nbad": 152, "tabs": 160}
-PIECES_ARGS_BYTES = 168
+               "expect": 128, "first_bad": 136, "nbad": 144, "tabs": 152}
 
 
 def pieces_kernarg(fields: dict, grid: int, threads: int) -> bytes:
-    ka = bytearray(424)
+    ka = bytearray(416)
     for k, v in fields.items():
         spec = PIECES_ARGS[k]
         o, fmt = spec if isinstance(spec, tuple) else (spec, "<Q")
         struct.pack_into(fmt, ka, o, v)
-    h = PIECES_ARGS_BYTES
-    struct.pack_into("<III", ka, h, grid, 1, 1)            # hidden_block_count_x/y/z
-    struct.pack_into("<HHH", ka, h + 12, threads, 1, 1)    # hidden_group_size_x/y/z
-    struct.pack_into("<H", ka, h + 64, 1)                  # hidden_grid_dims
+    struct.pack_into("<III", ka, 160, grid, 1, 1)        # hidden_block_count_x/y/z
+    struct.pack_into("<HHH", ka, 172, threads, 1, 1)     # hidden_group_size_x/y/z
+    struct.pack_into("<H", ka, 224, 1)                   # hidden_grid_dims
     return bytes(ka)
 
 
@@ -981,7 +979,7 @@ def launch(mem: Memory, asm: str, name: str, threads: int, lds_bytes: int, field
     wave-instructions executed.  Workgroups run to completion in order, so a dynamic (atomic-counter) schedule hands
     every item to the first workgroup -- functionally the same result, a different interleaving."""
     insns, labels = kernel_code(asm, name)
-    d_ka = mem.alloc(424, data=pieces_kernarg(fields, grid, threads))
+    d_ka = mem.alloc(416, data=pieces_kernarg(fields, grid, threads))
     steps = 0
     for g in (range(grid) if wgs is None else wgs):
         steps += Workgroup(mem, insns, labels, threads, lds_bytes, d_ka, g).run()

@@ -245,3 +245,20 @@ def test_two_ranks_config2_gathered_results():
     p = line["parity"]
     assert p["blocks_checked_vs_reference"] == 65536 and p["blocks_sampled_vs_oracle"] == 16
     assert p["mismatches"] == 0 and len(line["digests"]) == 2
+
+
+def test_bench_self_launch_two_ranks_config2():
+    """`python3 bench.py --gpus 2` with no launcher: bench.py starts both ranks itself (here both
+    on cuda:0 with gloo for the results, KVSEP_BENCH_SAME_DEVICE), and the line says n_gpus 2 / world_size 2 with every
+    block of the global batch checked against the reference."""
+    env = dict(os.environ, KVSEP_BENCH_SAME_DEVICE="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "2", "--steps", "3", "--warmup",
+           "1", "--no-cpu", "--roundtrip-gib", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["world_size"] == 2 and line["backend"] == "gloo", line
+    p = line["parity"]
+    assert p["blocks_checked_vs_reference"] == 65536 and p["mismatches"] == 0, p

@@ -27,8 +27,8 @@ sys.path.insert(0, PKG)
 
 # the shipped narrow-family templates (launch_batch_in in csrc/crc32c_device.hip): name, threads per workgroup
 SORTED = "_ZN5kvsep27crc32c_narrow_sorted_kernelILi4ELb1ELi1024ELb0ELi0ELb%dEEEvNS_10PiecesArgsE"
-NARROW16 = "_ZN5kvsep20crc32c_narrow_kernelILi4ELb1ELi1024ELb0ELi0ELb1ENS_7LdsFullELb%dELi0EEEvNS_10PiecesArgsE"
-NARROW8 = "_ZN5kvsep20crc32c_narrow_kernelILi4ELb1ELi512ELb1ELi0ELb1ENS_7LdsFullELb%dELi0EEEvNS_10PiecesArgsE"
+NARROW16 = "_ZN5kvsep20crc32c_narrow_kernelILi4ELb1ELi1024ELb0ELi0ELb1ENS_7LdsFullELb%dEEEvNS_10PiecesArgsE"
+NARROW8 = "_ZN5kvsep20crc32c_narrow_kernelILi4ELb1ELi512ELb1ELi0ELb1ENS_7LdsFullELb%dEEEvNS_10PiecesArgsE"
 KERNELS = [("sorted", SORTED, 1024), ("narrow16", NARROW16, 1024), ("narrow8", NARROW8, 512)]
 
 
