@@ -1580,66 +1580,12 @@ __global__ void __launch_bounds__(512) stream_read_kernel(uintptr_t src, uint64_
   if (acc == 0x9e3779b9u) atomicXor(sink, acc);  // keeps the loads live; practically never stores
 }
 
-#ifdef KVSEP_DIAG
-// Diagnostic (wrong results by design): does a read pattern keep its rate once every row goes through the CRC
-// kernel's Z_1024 fold chain?  kWgChunk: the ceiling's pattern above (the workgroup's waves interleave the rows of
-// one 1 MiB chunk); else per-wave contiguous 128 KiB chunks, round-robin (the CRC kernel's piece pattern).  Each lane
-// folds its 16 B per row into 4 chains through the replicated LDS table, as crc32c_pieces_kernel does.
-template <bool kWgChunk, int kRows>
-__global__ void __launch_bounds__(512) stream_fold_kernel(uintptr_t src, uint64_t n16, uint32_t* sink,
-                                                          const DevTables* tabs) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  fill_lds<512>(lds, &tabs->z1024[0][0], tabs, threadIdx.x);
-  __syncthreads();
-  const uint32_t lc0 = (lane & 31u) << 2, lc1 = lc0 | 0x10000u;
-  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-  if (kWgChunk) {
-    constexpr uint64_t kChunk = 1u << 20;
-    constexpr uint64_t kStep = 8 * kRows * kRowBytes;
-    const uint64_t nchunks = n16 * 16 / kChunk;
-    for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-      const uintptr_t p = src + c * kChunk + uintptr_t(w) * kRowBytes + lane * 16u;
-#pragma unroll 1
-      for (uint64_t r = 0; r < kChunk; r += kStep) {
-        uint4 v[kRows];
-#pragma unroll
-        for (int u = 0; u < kRows; ++u) v[u] = ld16<true>(p + r + uint64_t(u) * 8 * kRowBytes);
-#pragma unroll
-        for (int u = 0; u < kRows; ++u) {
-          c0 = fold_step(lds, c0, v[u].x, lc0, lc1);
-          c1 = fold_step(lds, c1, v[u].y, lc0, lc1);
-          c2 = fold_step(lds, c2, v[u].z, lc0, lc1);
-          c3 = fold_step(lds, c3, v[u].w, lc0, lc1);
-        }
-      }
-    }
-  } else {
-    constexpr uint64_t kChunk = 128u << 10;
-    const uint64_t nchunks = n16 * 16 / kChunk, nwaves = uint64_t(gridDim.x) * 8;
-    for (uint64_t c = uint64_t(w) * gridDim.x + blockIdx.x; c < nchunks; c += nwaves) {
-      const uintptr_t p = src + c * kChunk + lane * 16u;
-#pragma unroll 1
-      for (uint64_t r = 0; r < kChunk; r += kRows * kRowBytes) {
-        uint4 v[kRows];
-#pragma unroll
-        for (int u = 0; u < kRows; ++u) v[u] = ld16<true>(p + r + uint64_t(u) * kRowBytes);
-#pragma unroll
-        for (int u = 0; u < kRows; ++u) {
-          c0 = fold_step(lds, c0, v[u].x, lc0, lc1);
-          c1 = fold_step(lds, c1, v[u].y, lc0, lc1);
-          c2 = fold_step(lds, c2, v[u].z, lc0, lc1);
-          c3 = fold_step(lds, c3, v[u].w, lc0, lc1);
-        }
-      }
-    }
-  }
-  const uint32_t acc = c0 ^ c1 ^ c2 ^ c3;
-  if (acc == 0x9e3779b9u) atomicXor(sink, acc);
-}
-#endif
 
 }  // namespace kvsep
+
+#ifdef KVSEP_DIAG
+#include "crc32c_diag.inc"  // the tools build's A/B variants (never in the shipped library)
+#endif
 
 // ================================================================================================
 // host side
@@ -1845,56 +1791,20 @@ template <bool P, bool D, bool V>
 void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs& a) {
   // Default (1): 8-wave workgroups (2 waves per SIMD, up to 256 VGPRs), 4-row groups, non-temporal loads, next
   // item staged ahead.  On one MI355X, interleaved in one process (tools/ab_variants.py), 8 waves beat 16 waves
-  // by 1.5-2 % on 1 MiB blocks and by 4-5 % on the Zipf batch; 12 waves sit between.  The others are for A/B:
-  //   0: plain loads    2: no staging ahead    3: 8-row groups
-  // (a 3-slot ring of row groups, 8 rows in flight, was tried and measured -2 to -7 %: the extra VGPRs cost
-  // LDS-lookup overlap; so was staging items two ahead, -1.5 % on the Zipf batch)
-  //   5: 16-wave workgroups (the round-1 kernel)    6: 12-wave workgroups    7: 4-wave workgroups, 8-row groups
-  //   10: rows ending at the 16-B aligned end (before the 128-B grid)
-  //   22 / 24: 2- / 3-row groups; 23 / 25: 4- / 8-row groups folded before the next group loads (exact; measured
-  //   slower or equal)
-  //   8, 9, 11, 12: diagnostic ablations (wrong results): no lane merge, XOR folds, no head/tail steps, no tree
-  // Only the default is compiled into the shipped library; the rest exist in the KVSEP_DIAG tools build
-  // (`make -C kv-separate_amd diag` -> tools/libkvsep_diag.so).
+  // by 1.5-2 % on 1 MiB blocks and by 4-5 % on the Zipf batch; 12 waves sit between.  (A 3-slot ring of row groups,
+  // 8 rows in flight, was tried and measured -2 to -7 %: the extra VGPRs cost LDS-lookup overlap; so was staging items
+  // two ahead, -1.5 % on the Zipf batch.)  Only the default is compiled into the shipped library; the A/B and ablation
+  // variants live in crc32c_diag.inc, compiled into the KVSEP_DIAG tools build only.
   constexpr int T = kWgThreads;
   if (V) {  // the verify form: the shipped configuration only
     crc32c_pieces_kernel<P, D, 4, true, true, 0, T, true, true><<<grid, T, 0, s>>>(a);
     return;
   }
-  switch (variant) {
 #ifdef KVSEP_DIAG
-    case 0: crc32c_pieces_kernel<P, D, 4, false, true, 0, T><<<grid, T, 0, s>>>(a); break;
-    case 2: crc32c_pieces_kernel<P, D, 4, true, false, 0, T><<<grid, T, 0, s>>>(a); break;
-    case 3: crc32c_pieces_kernel<P, D, 8, true, true, 0, T><<<grid, T, 0, s>>>(a); break;
-    case 5: crc32c_pieces_kernel<P, D, 4, true, true, 0, 1024><<<grid, 1024, 0, s>>>(a); break;
-    case 6: crc32c_pieces_kernel<P, D, 4, true, true, 0, 768><<<grid, 768, 0, s>>>(a); break;
-    case 7: crc32c_pieces_kernel<P, D, 8, true, true, 0, 256><<<grid, 256, 0, s>>>(a); break;
-    case 8: crc32c_pieces_kernel<P, D, 4, true, true, 1, T><<<grid, T, 0, s>>>(a); break;  // ablation
-    case 9: crc32c_pieces_kernel<P, D, 4, true, true, 2, T><<<grid, T, 0, s>>>(a); break;  // ablation
-    case 10: crc32c_pieces_kernel<P, D, 4, true, true, 0, T, false><<<grid, T, 0, s>>>(a); break;  // 16-B rows
-    case 11: crc32c_pieces_kernel<P, D, 4, true, true, 3, T><<<grid, T, 0, s>>>(a); break;  // ablation: no head/tail
-    case 12: crc32c_pieces_kernel<P, D, 4, true, true, 4, T><<<grid, T, 0, s>>>(a); break;  // ablation: no lane tree
-    case 22: crc32c_pieces_kernel<P, D, 2, true, true, 0, T><<<grid, T, 0, s>>>(a); break;  // 2-row groups
-    case 23: crc32c_pieces_kernel<P, D, 4, true, true, 5, T><<<grid, T, 0, s>>>(a); break;  // unpipelined groups
-    case 24: crc32c_pieces_kernel<P, D, 3, true, true, 0, T><<<grid, T, 0, s>>>(a); break;  // 3-row groups
-    case 25: crc32c_pieces_kernel<P, D, 8, true, true, 5, T><<<grid, T, 0, s>>>(a); break;  // unpipelined, 8 rows
-    case 14:  // guided grabs of remaining / (d nwaves), d = 1, 2, 8, 16, 32, 4 (default: adaptive)
-    case 15:
-    case 17:
-    case 18:
-    case 19:
-    case 20:  // divisor 4 (the fixed divisor before the adaptive one)
-    case 21: {  // divisor 4, at most 64 items per grab
-      PiecesArgs b = a;
-      b.guided_div = variant == 14 ? 1 : variant == 15 ? 2 : variant == 17 ? 8 : variant == 18 ? 16 : variant == 19 ? 32
-                     : 4;
-      b.guided_cap = variant == 21 ? 64 : 0;
-      crc32c_pieces_kernel<P, D, 4, true, true, 0, T><<<grid, T, 0, s>>>(b);
-      break;
-    }
+  if (diag_launch_pieces<P, D>(variant, grid, s, a)) return;
 #endif
-    default: crc32c_pieces_kernel<P, D, 4, true, true, 0, T><<<grid, T, 0, s>>>(a); break;
-  }
+  (void)variant;
+  crc32c_pieces_kernel<P, D, 4, true, true, 0, T><<<grid, T, 0, s>>>(a);
 }
 
 template <bool V>
@@ -2029,55 +1939,10 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     } else {
     // diag variants 24-29 run their own in-kernel compare; every other diag variant gets verify_finish_kernel
     fused = !expect || (nv >= 24 && nv <= 29);
-    switch (nv) {
 #ifdef KVSEP_DIAG
-      case 2: crc32c_narrow_kernel<4, true, 512><<<grid, 512, 0, s>>>(a); break;
-      case 3: crc32c_narrow_kernel<4, true, 768><<<grid, 768, 0, s>>>(a); break;
-      case 4: crc32c_narrow_kernel<8, true, 512><<<grid, 512, 0, s>>>(a); break;
-      case 5: crc32c_narrow_kernel<8, true, 768><<<grid, 768, 0, s>>>(a); break;
-      case 12: crc32c_narrow_kernel<8, true, 512, true><<<grid, 512, 0, s>>>(a); break;
-      case 14: crc32c_narrow_kernel<4, true, 1024, true><<<grid, 1024, 0, s>>>(a); break;
-      case 16: crc32c_narrow_kernel<4, true, 1024, false, 1><<<grid, 1024, 0, s>>>(a); break;  // ablation
-      case 18: crc32c_narrow_kernel<4, true, 1024, false, 0, false><<<grid, 1024, 0, s>>>(a); break;  // 16-B rows
-      case 19: crc32c_narrow_kernel<4, true, 512, true, 0, false><<<grid, 512, 0, s>>>(a); break;     // 16-B rows
-      case 17: crc32c_narrow_kernel<4, true, 512, true, 1><<<grid, 512, 0, s>>>(a); break;    // ablation
-      case 21: crc32c_narrow_sorted_kernel<4, true, 512><<<grid, 512, 0, s>>>(a); break;
-      case 22: crc32c_narrow_sorted_kernel<4, true, 768><<<grid, 768, 0, s>>>(a); break;
-      case 23: crc32c_narrow_sorted_kernel<4, true, 1024, true><<<grid, 1024, 0, s>>>(a); break;  // drain per group
-      case 24: crc32c_narrow_sorted_kernel<4, true, 1024, false, 1><<<grid, 1024, 0, s>>>(a); break;  // compare inside
-      case 25: crc32c_narrow_sorted_kernel<4, true, 1024, false, 2><<<grid, 1024, 0, s>>>(a); break;  // load inside
-      case 26: crc32c_narrow_sorted_kernel<4, true, 1024, false, 3><<<grid, 1024, 0, s>>>(a); break;  // 24 + s_nops
-      case 27: crc32c_narrow_sorted_kernel<4, true, 1024, false, 4><<<grid, 1024, 0, s>>>(a); break;  // 24 + drain
-      case 28: crc32c_narrow_sorted_kernel<4, true, 1024, false, 5><<<grid, 1024, 0, s>>>(a); break;  // store, no atomics
-      case 29: crc32c_narrow_sorted_kernel<4, true, 1024, false, 6><<<grid, 1024, 0, s>>>(a); break;  // ballot compare
-      // compact 80 KiB LDS image (two workgroups per CU): 30 / 34: 8-wave workgroups, two per CU, persistent (34:
-      // fill overlapped); 31 / 35: one 8-block group per wave, grid over the whole batch (the dispatcher balances);
-      // 32: two groups per wave; 33: 16-wave workgroups, one per CU (the conflict cost alone)
-      case 30:
-      case 31:
-      case 32:
-      case 34:
-      case 35: {
-        const uint64_t groups = (count + 7) / 8;
-        const uint64_t per = nv == 31 || nv == 35 ? 8 : nv == 32 ? 16 : 0;
-        uint64_t g2 = 2ull * grid;
-        if (per && (groups + per - 1) / per > g2) g2 = (groups + per - 1) / per;
-        if (nv == 34 || nv == 35)
-          crc32c_narrow_kernel<4, true, 512, true, 0, true, LdsCompact><<<unsigned(g2), 512, 0, s>>>(a);
-        else
-          crc32c_narrow_kernel<4, true, 512, false, 0, true, LdsCompact><<<unsigned(g2), 512, 0, s>>>(a);
-        break;
-      }
-      case 33: crc32c_narrow_kernel<4, true, 1024, false, 0, true, LdsCompact><<<grid, 1024, 0, s>>>(a); break;
-      case 36: crc32c_narrow_kernel<2, true, 1024, false, 0, true, LdsCompact><<<grid, 1024, 0, s>>>(a); break;
-      case 37: crc32c_narrow_kernel<2, true, 1024><<<grid, 1024, 0, s>>>(a); break;
-      case 38: crc32c_narrow_kernel<4, true, 1024, true, 0, true, LdsCompact><<<grid, 1024, 0, s>>>(a); break;
-      // one wave per SIMD with deep row groups (no issue-age order between a SIMD's waves): 40 / 41: 4 waves, 16 /
-      // 8-row groups; 42: 4 waves, 16-row groups, fill overlapped (8 waves with 16-row groups spill)
-      case 40: crc32c_narrow_kernel<16, true, 256><<<grid, 256, 0, s>>>(a); break;
-      case 41: crc32c_narrow_kernel<8, true, 256><<<grid, 256, 0, s>>>(a); break;
-      case 42: crc32c_narrow_kernel<16, true, 256, true><<<grid, 256, 0, s>>>(a); break;
+    if (!diag_launch_narrow(nv, grid, s, a, count))
 #endif
+    switch (nv) {
       case 9: crc32c_narrow_kernel<4, true, 512, true><<<grid, 512, 0, s>>>(a); break;
       case 20: crc32c_narrow_sorted_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
       default: crc32c_narrow_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
