@@ -443,6 +443,18 @@ class Context:
                "kvsep_sst_trailers_host")
         return out[:k]
 
+    def sst_trailers_raw(self, addrs, lens, types, out):
+        """kvsep_sst_trailers_host on prebuilt arrays: addrs = uint64 host addresses of the blocks, lens their uint64
+        lengths, types uint8, out a uint32 array filled with the trailer words.  No per-block Python work."""
+        addrs = np.ascontiguousarray(addrs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        t = np.ascontiguousarray(types, dtype=np.uint8)
+        vp = ctypes.c_void_p
+        _check(lib().kvsep_sst_trailers_host(self._h, addrs.ctypes.data_as(vp), lens.ctypes.data_as(vp),
+                                             t.ctypes.data_as(vp), out.ctypes.data_as(vp), lens.size),
+               "kvsep_sst_trailers_host")
+        return out
+
     def sst_verify(self, image, off, length):
         """table/format.cc:73-108 for every block handle (off, length) of a host SST file image -> (out, first_bad,
         nbad): out[i] = Value(block, len + 1); first_bad = -1 when every block matches its stored trailer word."""

@@ -179,6 +179,40 @@ def main():
     rows.append(row("sst_verify", "table/format.cc:99-108", count * (blen + 1), dt, clean and caught,
                     f"{count} blocks + type bytes of a device-resident file image: Value(block, n+1) vs Unmask(stored); "
                     f"parity: clean image passes, one flipped bit is reported at block {count // 3}"))
+
+    # ---- the same two call sites for host-resident blocks (kvsep_sst_trailers_host / kvsep_sst_verify_host): the way
+    # TableBuilder::WriteRawBlock and ReadBlock hold them, through the pinned staging pipeline (PCIe-inclusive)
+    t8[count // 3, 100] ^= 1  # intact again
+    ver()
+    torch.cuda.synchronize()
+    dout = out.cpu().numpy().view(np.uint32).copy()  # the device form's words on the intact image
+    himg = fimg[:span].cpu().numpy()  # pageable host copy of the file image (blocks + trailers)
+    addrs = np.uint64(himg.ctypes.data) + off  # the blocks where TableBuilder holds them: prebuilt pointers
+    hty = ty.copy()
+    words = np.zeros(count, np.uint32)
+    dt, _ = timed(lambda: ctx.sst_trailers_raw(addrs, lens, hty, words), 3)
+    okh = np.array_equal(words, mk)
+    views = [memoryview(himg)[int(o):int(o) + blen] for o in off[:64]]  # the per-block Python form agrees too
+    okh = okh and np.array_equal(ctx.sst_trailers(views, hty[:64]), mk[:64])
+    rows.append(row("sst_trailers_host", "table/table_builder.cc:209-232", count * blen, dt, okh,
+                    f"{count} x {blen} B pageable host blocks (one pointer per block) -> trailer words, H2D + kernel + "
+                    "D2H; parity: equal to the device form's words"))
+    res = None
+
+    def hver():
+        nonlocal res
+        res = ctx.sst_verify(himg, off, lens)
+
+    dt, _ = timed(hver, 3)
+    hout, hfb, hnb = res
+    okv = hfb == -1 and hnb == 0 and np.array_equal(hout, dout)
+    himg[int(off[count // 5]) + 7] ^= 4
+    _, hfb2, hnb2 = ctx.sst_verify(himg, off, lens)
+    okv = okv and hfb2 == count // 5 and hnb2 == 1
+    rows.append(row("sst_verify_host", "table/format.cc:73-108", count * (blen + 1), dt, okv,
+                    f"a pageable {span >> 20} MiB host file image with {count} block handles -> Value(block, n+1) vs "
+                    f"Unmask(stored), H2D + kernel + D2H; parity: clean image passes with the device form's words, one "
+                    f"flipped bit is reported at block {count // 5}"))
     ctx.close()
     if args.out:
         with open(args.out, "w") as f:
