@@ -12,6 +12,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <thread>
+#include <utility>
 #include <vector>
 #include <chrono>
 #include <cstdint>
@@ -40,13 +41,25 @@ class CopyPool {
     cv_.notify_all();
     for (auto& t : th_) t.join();
   }
-  // Chunks of <= 1 MiB are claimed from one counter by the workers and the caller alike.
+  // Chunks of <= 1 MiB, grouped into units of >= 256 KiB of consecutive chunks, are claimed from one counter by the
+  // workers and the caller alike.  A claim per unit, not per chunk: 16 K blocks of 4 KiB were 16 K claims on one
+  // counter line per 64 MiB slot, and the gather ran at half the PCIe rate.
   void run(const CopySeg* segs, uint64_t nseg) {
     chunks_.clear();
+    units_.clear();
+    uint64_t acc = 0, first = 0;
     for (uint64_t i = 0; i < nseg; ++i)
-      for (uint64_t o = 0; o < segs[i].n; o += kChunk)
-        chunks_.push_back({segs[i].dst + o, segs[i].src + o, std::min<uint64_t>(kChunk, segs[i].n - o)});
-    if (chunks_.size() <= 2 || th_.empty()) {  // not worth waking anyone
+      for (uint64_t o = 0; o < segs[i].n; o += kChunk) {
+        const uint64_t n = std::min<uint64_t>(kChunk, segs[i].n - o);
+        chunks_.push_back({segs[i].dst + o, segs[i].src + o, n});
+        if ((acc += n) >= kUnit) {
+          units_.push_back({first, chunks_.size()});
+          first = chunks_.size();
+          acc = 0;
+        }
+      }
+    if (first < chunks_.size()) units_.push_back({first, chunks_.size()});
+    if (units_.size() <= 2 || th_.empty()) {  // not worth waking anyone
       for (auto& c : chunks_) std::memcpy(c.dst, c.src, c.n);
       return;
     }
@@ -64,8 +77,11 @@ class CopyPool {
 
  private:
   static constexpr uint64_t kChunk = 1ull << 20;
+  static constexpr uint64_t kUnit = 256ull << 10;
   void drain() {
-    for (uint64_t k; (k = next_.fetch_add(1)) < chunks_.size();) std::memcpy(chunks_[k].dst, chunks_[k].src, chunks_[k].n);
+    for (uint64_t k; (k = next_.fetch_add(1)) < units_.size();)
+      for (uint64_t c = units_[k].first; c < units_[k].second; ++c)
+        std::memcpy(chunks_[c].dst, chunks_[c].src, chunks_[c].n);
   }
   void worker() {
     uint64_t seen = 0;
@@ -83,6 +99,7 @@ class CopyPool {
   }
   std::vector<std::thread> th_;
   std::vector<CopySeg> chunks_;
+  std::vector<std::pair<uint64_t, uint64_t>> units_;  // [first, end) chunk ranges claimed as one
   std::atomic<uint64_t> next_{0};
   std::mutex m_;
   std::condition_variable cv_, done_cv_;
