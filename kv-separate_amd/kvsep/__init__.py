@@ -449,6 +449,11 @@ class Context:
         addrs = np.ascontiguousarray(addrs, dtype=np.uint64)
         lens = np.ascontiguousarray(lens, dtype=np.uint64)
         t = np.ascontiguousarray(types, dtype=np.uint8)
+        if addrs.size != lens.size or t.size != lens.size:
+            raise ValueError("addrs, lens and types must have the same length")
+        if not (isinstance(out, np.ndarray) and out.dtype == np.uint32 and out.flags.c_contiguous
+                and out.size >= lens.size):
+            raise ValueError("out must be a contiguous uint32 array with room for every block")
         vp = ctypes.c_void_p
         _check(lib().kvsep_sst_trailers_host(self._h, addrs.ctypes.data_as(vp), lens.ctypes.data_as(vp),
                                              t.ctypes.data_as(vp), out.ctypes.data_as(vp), lens.size),
