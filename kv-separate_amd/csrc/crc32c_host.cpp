@@ -27,87 +27,6 @@
 
 namespace kvsep {
 
-// ------------------------------------------------------------------ parallel staging copies
-class CopyPool {
- public:
-  explicit CopyPool(int nthreads) {
-    for (int i = 0; i < nthreads; ++i) th_.emplace_back([this] { worker(); });
-  }
-  ~CopyPool() {
-    {
-      std::lock_guard<std::mutex> g(m_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
-  }
-  // Chunks of <= 1 MiB, grouped into units of >= 256 KiB of consecutive chunks, are claimed from one counter by the
-  // workers and the caller alike.  A claim per unit, not per chunk: 16 K blocks of 4 KiB were 16 K claims on one
-  // counter line per 64 MiB slot, and the gather ran at half the PCIe rate.
-  void run(const CopySeg* segs, uint64_t nseg) {
-    chunks_.clear();
-    units_.clear();
-    uint64_t acc = 0, first = 0;
-    for (uint64_t i = 0; i < nseg; ++i)
-      for (uint64_t o = 0; o < segs[i].n; o += kChunk) {
-        const uint64_t n = std::min<uint64_t>(kChunk, segs[i].n - o);
-        chunks_.push_back({segs[i].dst + o, segs[i].src + o, n});
-        if ((acc += n) >= kUnit) {
-          units_.push_back({first, chunks_.size()});
-          first = chunks_.size();
-          acc = 0;
-        }
-      }
-    if (first < chunks_.size()) units_.push_back({first, chunks_.size()});
-    if (units_.size() <= 2 || th_.empty()) {  // not worth waking anyone
-      for (auto& c : chunks_) std::memcpy(c.dst, c.src, c.n);
-      return;
-    }
-    {
-      std::lock_guard<std::mutex> g(m_);
-      next_.store(0);
-      active_ = int(th_.size());
-      ++gen_;
-    }
-    cv_.notify_all();
-    drain();
-    std::unique_lock<std::mutex> lk(m_);
-    done_cv_.wait(lk, [this] { return active_ == 0; });
-  }
-
- private:
-  static constexpr uint64_t kChunk = 1ull << 20;
-  static constexpr uint64_t kUnit = 256ull << 10;
-  void drain() {
-    for (uint64_t k; (k = next_.fetch_add(1)) < units_.size();)
-      for (uint64_t c = units_[k].first; c < units_[k].second; ++c)
-        std::memcpy(chunks_[c].dst, chunks_[c].src, chunks_[c].n);
-  }
-  void worker() {
-    uint64_t seen = 0;
-    for (;;) {
-      {
-        std::unique_lock<std::mutex> lk(m_);
-        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-        if (stop_) return;
-        seen = gen_;
-      }
-      drain();
-      std::lock_guard<std::mutex> g(m_);
-      if (--active_ == 0) done_cv_.notify_one();
-    }
-  }
-  std::vector<std::thread> th_;
-  std::vector<CopySeg> chunks_;
-  std::vector<std::pair<uint64_t, uint64_t>> units_;  // [first, end) chunk ranges claimed as one
-  std::atomic<uint64_t> next_{0};
-  std::mutex m_;
-  std::condition_variable cv_, done_cv_;
-  uint64_t gen_ = 0;
-  int active_ = 0;
-  bool stop_ = false;
-};
-
 CopyPool* copy_pool_create() {
   int n = 7;  // + the caller: 8 copiers
   if (const char* v = std::getenv("KVSEP_COPY_THREADS")) n = std::max(0, std::atoi(v) - 1);

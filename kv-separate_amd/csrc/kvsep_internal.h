@@ -6,6 +6,8 @@
 #include <cstdint>
 #include <mutex>
 
+#include "copy_pool.h"
+
 struct kvsep_crc32c_ctx;
 
 namespace kvsep {
@@ -33,14 +35,7 @@ struct Scratch {
 };
 void free_scratch(Scratch& sc);
 
-// Persistent host threads that copy pageable data into the pinned staging slots in parallel: one thread's
-// memcpy (~10-25 GB/s) is below the PCIe Gen5 x16 rate the slots are drained at (~55 GB/s).
-class CopyPool;
-struct CopySeg {
-  uint8_t* dst;
-  const uint8_t* src;
-  uint64_t n;
-};
+// The persistent host copiers of the staging pipeline (copy_pool.h).
 CopyPool* copy_pool_create();
 void copy_pool_destroy(CopyPool* p);
 void copy_pool_run(CopyPool* p, const CopySeg* segs, uint64_t nseg);  // returns when every byte is copied
