@@ -18,6 +18,7 @@ struct CopySeg {
   uint8_t* dst;
   const uint8_t* src;
   uint64_t n;
+  uint8_t* dst2 = nullptr;  // optional second destination ("tee"): the bytes also land here, read from cache
 };
 
 class CopyPool {
@@ -43,7 +44,7 @@ class CopyPool {
     for (uint64_t i = 0; i < nseg; ++i)
       for (uint64_t o = 0; o < segs[i].n; o += kChunk) {
         const uint64_t n = std::min<uint64_t>(kChunk, segs[i].n - o);
-        chunks_.push_back({segs[i].dst + o, segs[i].src + o, n});
+        chunks_.push_back({segs[i].dst + o, segs[i].src + o, n, segs[i].dst2 ? segs[i].dst2 + o : nullptr});
         if ((acc += n) >= kUnit) {
           units_.push_back({first, chunks_.size()});
           first = chunks_.size();
@@ -52,7 +53,7 @@ class CopyPool {
       }
     if (first < chunks_.size()) units_.push_back({first, chunks_.size()});
     if (units_.size() <= 2 || th_.empty()) {  // not worth waking anyone
-      for (auto& c : chunks_) std::memcpy(c.dst, c.src, c.n);
+      for (auto& c : chunks_) copy(c);
       return;
     }
     {
@@ -70,10 +71,21 @@ class CopyPool {
  private:
   static constexpr uint64_t kChunk = 1ull << 20;
   static constexpr uint64_t kUnit = 256ull << 10;
+  static constexpr uint64_t kTee = 64ull << 10;  // a tee copies 64 KiB to dst, then the same 64 KiB (cached) to dst2
+  static void copy(const CopySeg& c) {
+    if (!c.dst2) {
+      std::memcpy(c.dst, c.src, c.n);
+      return;
+    }
+    for (uint64_t o = 0; o < c.n; o += kTee) {
+      const uint64_t m = std::min(kTee, c.n - o);
+      std::memcpy(c.dst + o, c.src + o, m);
+      std::memcpy(c.dst2 + o, c.dst + o, m);
+    }
+  }
   void drain() {
     for (uint64_t k; (k = next_.fetch_add(1)) < units_.size();)
-      for (uint64_t c = units_[k].first; c < units_[k].second; ++c)
-        std::memcpy(chunks_[c].dst, chunks_[c].src, chunks_[c].n);
+      for (uint64_t c = units_[k].first; c < units_[k].second; ++c) copy(chunks_[c]);
   }
   void worker() {
     uint64_t seen = 0;

@@ -327,6 +327,72 @@ int host_copy_parallel(kvsep_crc32c_ctx* c, char* const* dst, const char* const*
   return KVSEP_OK;
 }
 
+// The pointer-per-block host form (kvsep_crc32c_batch_host), optionally with a tee: tee[i] != nullptr also receives
+// record i's bytes, copied by the same gather that stages them for the GPU (one read of the source, two writes),
+// so a framing writer needs no second pass over its payloads (kvsep_log_frame_host).
+int batch_host_tee(kvsep_crc32c_ctx* c, const uint32_t* init, const char* const* ptr, const uint64_t* len,
+                   uint32_t* out, uint64_t count, char* const* tee) {
+  if (!c || (count && (!ptr || !len || !out))) {
+    set_last_error("null argument");
+    return KVSEP_EINVAL;
+  }
+  std::lock_guard<std::mutex> g(ctx_mutex(c));
+  int rc = ensure_staging(c);
+  if (rc) return rc;
+  DeviceGuard dg(ctx_device(c));
+  if (dg.err != hipSuccess) return hip_fail("hipSetDevice", dg.err);
+  HostStaging& s = ctx_staging(c);
+  SlotJob jobs[HostStaging::kSlots];
+  int slot = 0;
+  uint64_t i = 0;
+  while (i < count) {
+    if (len[i] > s.bytes) {
+      uint32_t r = 0;
+      rc = big_block(c, s, jobs, out, reinterpret_cast<const uint8_t*>(ptr[i]), len[i], init ? init[i] : 0u,
+                     is_pinned(ptr[i]), &r);
+      if (rc) return rc;
+      out[i] = r;
+      if (tee && tee[i]) {  // a record over the slot size is staged in pieces: its tee copy is one pass of its own
+        const CopySeg cs{reinterpret_cast<uint8_t*>(tee[i]), reinterpret_cast<const uint8_t*>(ptr[i]), len[i]};
+        copy_pool_run(s.pool, &cs, 1);
+      }
+      ++i;
+      continue;
+    }
+    rc = retire(s, slot, jobs[slot], out);
+    if (rc) return rc;
+    uint64_t used = 0, j = i, max_len = 0;
+    // gather: blocks packed back to back, each at a 16-B aligned staging offset (copied by the pool below)
+    std::vector<CopySeg> segs;
+    while (j < count && j - i < s.max_blocks && len[j] <= s.bytes) {
+      const uint64_t at = (used + 15) & ~uint64_t(15);
+      if (at + len[j] > s.bytes) break;
+      if (len[j])
+        segs.push_back({s.h_data[slot] + at, reinterpret_cast<const uint8_t*>(ptr[j]), len[j],
+                        tee ? reinterpret_cast<uint8_t*>(tee[j]) : nullptr});
+      s.h_desc[slot][j - i] = at;
+      s.h_desc[slot][s.max_blocks + (j - i)] = len[j];
+      if (init) s.h_init[slot][j - i] = init[j];
+      max_len = std::max(max_len, len[j]);
+      used = at + len[j];
+      ++j;
+    }
+    copy_pool_run(s.pool, segs.data(), segs.size());
+    rc = submit(c, s, slot, j - i, used, max_len, nullptr, init != nullptr);
+    if (rc) return rc;
+    jobs[slot].busy = true;
+    jobs[slot].first = i;
+    jobs[slot].n = j - i;
+    slot ^= 1;
+    i = j;
+  }
+  for (int k = 0; k < HostStaging::kSlots; ++k) {
+    rc = retire(s, k, jobs[k], out);
+    if (rc) return rc;
+  }
+  return KVSEP_OK;
+}
+
 }  // namespace kvsep
 
 using namespace kvsep;
@@ -461,59 +527,7 @@ int kvsep_crc32c_batch_host_span(kvsep_crc32c_ctx* c, const char* host_base, uin
 
 int kvsep_crc32c_batch_host(kvsep_crc32c_ctx* c, const uint32_t* init, const char* const* ptr, const uint64_t* len,
                             uint32_t* out, uint64_t count) {
-  if (!c || (count && (!ptr || !len || !out))) {
-    set_last_error("null argument");
-    return KVSEP_EINVAL;
-  }
-  std::lock_guard<std::mutex> g(ctx_mutex(c));
-  int rc = ensure_staging(c);
-  if (rc) return rc;
-  DeviceGuard dg(ctx_device(c));
-  if (dg.err != hipSuccess) return hip_fail("hipSetDevice", dg.err);
-  HostStaging& s = ctx_staging(c);
-  SlotJob jobs[HostStaging::kSlots];
-  int slot = 0;
-  uint64_t i = 0;
-  while (i < count) {
-    if (len[i] > s.bytes) {
-      uint32_t r = 0;
-      rc = big_block(c, s, jobs, out, reinterpret_cast<const uint8_t*>(ptr[i]), len[i], init ? init[i] : 0u,
-                     is_pinned(ptr[i]), &r);
-      if (rc) return rc;
-      out[i] = r;
-      ++i;
-      continue;
-    }
-    rc = retire(s, slot, jobs[slot], out);
-    if (rc) return rc;
-    uint64_t used = 0, j = i, max_len = 0;
-    // gather: blocks packed back to back, each at a 16-B aligned staging offset (copied by the pool below)
-    std::vector<CopySeg> segs;
-    while (j < count && j - i < s.max_blocks && len[j] <= s.bytes) {
-      const uint64_t at = (used + 15) & ~uint64_t(15);
-      if (at + len[j] > s.bytes) break;
-      if (len[j]) segs.push_back({s.h_data[slot] + at, reinterpret_cast<const uint8_t*>(ptr[j]), len[j]});
-      s.h_desc[slot][j - i] = at;
-      s.h_desc[slot][s.max_blocks + (j - i)] = len[j];
-      if (init) s.h_init[slot][j - i] = init[j];
-      max_len = std::max(max_len, len[j]);
-      used = at + len[j];
-      ++j;
-    }
-    copy_pool_run(s.pool, segs.data(), segs.size());
-    rc = submit(c, s, slot, j - i, used, max_len, nullptr, init != nullptr);
-    if (rc) return rc;
-    jobs[slot].busy = true;
-    jobs[slot].first = i;
-    jobs[slot].n = j - i;
-    slot ^= 1;
-    i = j;
-  }
-  for (int k = 0; k < HostStaging::kSlots; ++k) {
-    rc = retire(s, k, jobs[k], out);
-    if (rc) return rc;
-  }
-  return KVSEP_OK;
+  return kvsep::batch_host_tee(c, init, ptr, len, out, count, nullptr);
 }
 
 void* kvsep_host_alloc_pinned(uint64_t bytes) {

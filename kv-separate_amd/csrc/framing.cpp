@@ -21,6 +21,9 @@ namespace kvsep {
 // crc32c_host.cpp: copies dst[i] <- src[i] (n[i] bytes) on the context's copier threads.
 int host_copy_parallel(kvsep_crc32c_ctx* c, char* const* dst, const char* const* src, const uint64_t* n,
                        uint64_t count);
+// crc32c_host.cpp: kvsep_crc32c_batch_host whose gather also copies record i to tee[i] (one read of each payload).
+int batch_host_tee(kvsep_crc32c_ctx* c, const uint32_t* init, const char* const* ptr, const uint64_t* len,
+                   uint32_t* out, uint64_t count, char* const* tee);
 }  // namespace kvsep
 
 namespace {
@@ -95,6 +98,9 @@ int kvsep_vlog_frame_host(kvsep_crc32c_ctx* ctx, const char* const* payload, con
   }
   if (written) *written = need;
   if (need > dst_cap || (need && !dst)) return KVSEP_EINVAL;
+  // Checksums first, then the payload copy into the framed image as a pass of its own.  For ~1 MiB group-commit
+  // payloads that measured faster than copying each payload into the image from the gather that stages it (the
+  // tee that the log writer's <= 32 KiB fragments use): 36.5 vs 31.3 GiB/s, medians of three alternating runs.
   std::vector<uint32_t> crc(count);
   if (count) {
     const int rc = kvsep_crc32c_batch_host(ctx, nullptr, payload, len, crc.data(), count);
@@ -102,7 +108,7 @@ int kvsep_vlog_frame_host(kvsep_crc32c_ctx* ctx, const char* const* payload, con
   }
   uint64_t p = 0;
   std::vector<char*> at(count);
-  for (uint64_t i = 0; i < count; ++i) {  // db/value_log_writer.cc:57-70
+  for (uint64_t i = 0; i < count; ++i) {  // db/value_log_writer.cc:57-70: [masked crc LE32][len LE32]
     put_le32(dst + p, kvsep_crc32c_mask(crc[i]));
     put_le32(dst + p + 4, uint32_t(len[i]));
     at[i] = dst + p + kVlogHeader;
@@ -203,21 +209,23 @@ int kvsep_log_frame_host(kvsep_crc32c_ctx* ctx, const char* const* payload, cons
     flen[i] = frags[i].len;
     init[i] = type_crc[frags[i].type];
   }
+  // the fragment bytes land in dst from the same gather that stages them for the checksum (a tee: one read each;
+  // 36.0 vs 24.1 GiB/s against a second copy pass, medians of three alternating runs on one box)
+  std::vector<char*> at(nf);
+  for (uint64_t i = 0; i < nf; ++i) at[i] = dst + frags[i].at + kLogHeader;
   if (nf) {
-    const int rc = kvsep_crc32c_batch_host(ctx, init.data(), src.data(), flen.data(), crc.data(), nf);
+    const int rc = kvsep::batch_host_tee(ctx, init.data(), src.data(), flen.data(), crc.data(), nf, at.data());
     if (rc) return rc;
   }
   for (const auto& t : trailers) std::memset(dst + t.first, 0, t.second);
-  std::vector<char*> at(nf);
   for (uint64_t i = 0; i < nf; ++i) {  // EmitPhysicalRecord (:84-115)
     char* h = dst + frags[i].at;
     put_le32(h, kvsep_crc32c_mask(crc[i]));
     h[4] = char(frags[i].len & 0xff);
     h[5] = char(frags[i].len >> 8);
     h[6] = char(frags[i].type);
-    at[i] = h + kLogHeader;
   }
-  return kvsep::host_copy_parallel(ctx, at.data(), src.data(), flen.data(), nf);  // the fragment bytes
+  return KVSEP_OK;
 }
 
 int kvsep_sst_trailers_host(kvsep_crc32c_ctx* ctx, const char* const* block, const uint64_t* len, const uint8_t* types,

@@ -90,6 +90,10 @@ struct DeviceGuard {
 int device_batch_locked(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* base, const uint64_t* off,
                         const uint64_t* len, const uint32_t* init, uint32_t* out, uint64_t count,
                         uint64_t total_bytes, uint64_t max_len);
+// kvsep_crc32c_batch_host with an optional tee: tee[i] (when tee and tee[i] are non-null) also receives record i's bytes
+// from the gather that stages them (crc32c_host.cpp).  Takes the context's mutex.
+int batch_host_tee(kvsep_crc32c_ctx* c, const uint32_t* init, const char* const* ptr, const uint64_t* len,
+                   uint32_t* out, uint64_t count, char* const* tee);
 HostStaging& ctx_staging(kvsep_crc32c_ctx* c);
 std::mutex& ctx_mutex(kvsep_crc32c_ctx* c);
 int ctx_device(kvsep_crc32c_ctx* c);

@@ -66,7 +66,10 @@ def main():
     ap.add_argument("--log-gib", type=float, default=1.0)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--lib", default=None, help="another build of libkvsep_crc32c.so (A/B runs)")
     args = ap.parse_args()
+    if args.lib:
+        kvsep.LIB_PATH, kvsep._lib = args.lib, None
     oracle = load_oracle()
     ctx = kvsep.Context(0)
     rows = []

@@ -50,6 +50,12 @@ int host_copy_parallel(kvsep_crc32c_ctx*, char* const* dst, const char* const* s
     if (n[i]) std::memcpy(dst[i], src[i], n[i]);
   return KVSEP_OK;
 }
+int batch_host_tee(kvsep_crc32c_ctx* c, const uint32_t* init, const char* const* ptr, const uint64_t* len,
+                   uint32_t* out, uint64_t count, char* const* tee) {
+  for (uint64_t i = 0; i < count; ++i)
+    if (tee && tee[i] && len[i]) std::memcpy(tee[i], ptr[i], len[i]);
+  return kvsep_crc32c_batch_host(c, init, ptr, len, out, count);
+}
 }  // namespace kvsep
 
 int main() {
