@@ -140,3 +140,19 @@ def test_partition_byte_balanced():
                 assert abs(got - share) <= int(ln.max()), (count, parts, p, got, share)
     b = kvsep.partition(np.array([10, 0, 0, 10], np.uint64), 2)
     assert b.tolist() in ([0, 1, 4], [0, 2, 4], [0, 3, 4])
+
+
+def test_host_extend_lane_boundaries(oracle):
+    """The host leg's 3-way loop runs lanes of 4 KiB, 1 KiB and 256 B (crc32c_host.cpp host_crc): every length around
+    3 L for each L, and a sweep to 13 KB, at eight start offsets and two inits, against the oracle."""
+    data = splitmix64_bytes(60000, 77, 0)
+    lens = set(range(0, 13000, 37))
+    for L in (256, 1024, 4096):
+        for k in (1, 2, 3, 4):
+            lens.update(range(3 * L * k - 9, 3 * L * k + 10))
+    f = kvsep.lib().kvsep_crc32c_extend_host
+    for o in range(8):
+        for n in sorted(lens):
+            for init in (0, 0x9E3779B9):
+                b = data[o:o + n].tobytes()
+                assert f(init, data.ctypes.data + o, n) == oracle.extend(init, b), (o, n, init)
