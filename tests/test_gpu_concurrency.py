@@ -15,6 +15,10 @@ from kvsep import splitmix64_bytes
 
 pytestmark = pytest.mark.gpu
 
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no GPU", allow_module_level=True)
+
 
 def test_concurrent_dropin_and_host_forms(oracle):
     lib = kvsep.lib()
