@@ -12,6 +12,9 @@ import torch  # noqa: E402
 import kvsep  # noqa: E402
 from kvsep import workloads as W  # noqa: E402
 
+if os.environ.get("KVSEP_LIB"):  # another build of the library (A/B of the data generator)
+    kvsep.LIB_PATH, kvsep._lib = os.environ["KVSEP_LIB"], None
+
 count = 32768
 off, ln = W.cfg3_layout(count=count)
 span = int(off[-1] + ln[-1])
@@ -44,3 +47,6 @@ run("B")
 kvsep.fill_splitmix64(bufs["A"].data_ptr(), span, 99, 0)
 torch.cuda.synchronize()
 run("A")
+kvsep.fill_splitmix64(bufs["B"].data_ptr(), span, 98, 0)
+torch.cuda.synchronize()
+run("B")
