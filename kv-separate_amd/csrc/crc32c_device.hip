@@ -1536,10 +1536,17 @@ __device__ __forceinline__ uint64_t splitmix_word(uint64_t seed, uint64_t j) {
 }
 
 // Fast path: dst 16-B aligned and stream_offset % 16 == 0; each thread writes 16 B per step.
+// Non-temporal stores: the data goes to HBM without staying dirty in the caches.  With plain stores the first CRC
+// pass over a freshly generated batch ran ~5 % slower than the next ones (round 1's "first-pass effect", which config 5
+// paid on every slice it regenerates); with nt stores the first pass runs at the later passes' rate
+// (tools/cold_probe.py, profiles/round3/cold_first_pass_nt.log).
 __global__ void fill_splitmix_fast_kernel(uint4* dst, uint64_t n16, uint64_t seed, uint64_t w0) {
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
   for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n16; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint64_t lo = splitmix_word(seed, w0 + 2 * i), hi = splitmix_word(seed, w0 + 2 * i + 1);
-    dst[i] = make_uint4(uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32));
+    const v4u v = {uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32)};
+    __builtin_nontemporal_store(v, reinterpret_cast<__attribute__((address_space(1))) v4u*>(
+                                       reinterpret_cast<uintptr_t>(dst + i)));
   }
 }
 
