@@ -13,9 +13,10 @@ config 3 of BASELINE.json, 65,536 x 1 MiB blocks (64 GiB) per GPU (`--config 3a`
 N > 1: one process per GPU, each rank checksums its own shard; no data-path collective.  The ranks come from torchrun,
 or -- `bench.py --gpus N` with no WORLD_SIZE in the environment -- from bench.py itself (launch_ranks), over RCCL.
 
-Outside the timed region: RCCL all-gather of every rank's u32 results (4 B per block) and a check of EVERY block
-against the reference's whole-batch outputs (tests/golden/full_cfg*.u32, computed by the compiled util/crc32c.cc)
-where they cover it, an oracle recompute of sampled blocks elsewhere; the read-only streaming ceiling; the host
+Outside the timed region: RCCL all-gather of every rank's u32 results (4 B per block) and a check of EVERY block of
+every rank against the reference's whole-batch outputs (tests/golden/full_cfg*.u32 per block at up to 8 ranks;
+config 4 beyond its first 2^20 blocks by the reference's per-rank digests, full_cfg4_ranks.json -- all computed by the
+compiled util/crc32c.cc); the read-only streaming ceiling; the host
 round-trip rate; and -- rank 0 at N = 1 -- the compiled reference's CPU throughput on a bounded sample
 (cpu_baseline) at 1 thread and at every core this process may run on.
 """
@@ -63,6 +64,17 @@ def _cfg4_global(world):
     return _CFG4[world]
 
 
+def _cfg4_digest(world, rank):
+    """The reference's crc_of_crcs over this rank's block range of the N-rank config-4 batch
+    (tests/golden/full_cfg4_ranks.json, make_fullsize_golden.py): 8 Mi blocks of u32s are too many to commit."""
+    path = os.path.join(GOLDEN, "full_cfg4_ranks.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        parts = json.load(f)["ranks"].get(str(world))
+    return parts[rank] if parts else None
+
+
 class Plan:
     """What this rank checksums: a local block layout over one buffer, and one (stream_base, index_base) per pass
     -- the global stream offset of the buffer's first byte and the global index of its first block."""
@@ -70,7 +82,8 @@ class Plan:
     def __init__(self, cfg: str, world: int, rank: int):
         self.cfg = cfg
         self.passes = [(0, 0)]
-        self.golden = None  # (file, seed): reference per-block CRCs of the global batch, indexed globally
+        self.golden = None  # file of the reference's per-block CRCs of the global batch, indexed globally
+        self.digest = None  # {lo, hi, crc_of_crcs}: the reference's digest of this rank's block range
         if cfg in ("2", "3a", "3b"):
             if cfg == "2":
                 self.off, self.ln = W.cfg2_layout()
@@ -92,6 +105,7 @@ class Plan:
             self.off, self.ln, base, ib = shard.partition_layout(goff, glen, world, rank)
             self.passes = [(base, ib)]
             self.seed, self.golden = W.SEED + 2, "full_cfg4.u32"
+            self.digest = _cfg4_digest(world, rank)
             self.desc = (f"{world} x 1,048,576 Zipf(1.1) blocks, 32 B - 4 MiB, one batch cut into byte-balanced block "
                          f"ranges (config 4)")
             self.scaling = "weak"
@@ -245,9 +259,11 @@ def roundtrip_time(ctx, state, reps=3):
 
 
 def check_results(plan_all, results, oracle):
-    """Every rank's u32 results (gathered) against the reference's whole-batch outputs where they cover the block's
-    global index, an oracle recompute of 16 sampled blocks per (rank, pass) elsewhere.  Rank 0, untimed."""
-    checked = mism = sampled = 0
+    """Every rank's u32 results (gathered), rank 0, untimed: per block against the reference's whole-batch outputs
+    where the golden file covers the block's global index (configs 2 / 3a / 3b / 5 at up to 8 ranks, config 4's first
+    2^20 blocks); where it does not, the rank's whole range against the reference's digest of it (config 4 at N > 1);
+    an oracle recompute of 16 sampled blocks per (rank, pass) only where neither exists."""
+    checked = by_digest = mism = bad_ranges = sampled = total = 0
     gold_cache = {}
     for plan, res in zip(plan_all, results):
         k = plan.count
@@ -256,16 +272,28 @@ def check_results(plan_all, results, oracle):
             gold = gold_cache.setdefault(plan.golden, np.fromfile(os.path.join(GOLDEN, plan.golden), dtype="<u4"))
         for p, (base, ib) in enumerate(plan.passes):
             got = res[p * k:(p + 1) * k]
+            total += k
             n_gold = 0 if gold is None else max(0, min(k, gold.size - ib))
             if n_gold:
                 mism += int(np.count_nonzero(got[:n_gold] != gold[ib:ib + n_gold]))
                 checked += n_gold
+            if n_gold == k:
+                continue
+            dg = plan.digest
+            if dg is not None and dg["lo"] == ib and dg["hi"] == ib + k:
+                by_digest += k - n_gold
+                if shard.crc_of_crcs(got, kvsep.extend_host) != dg["crc_of_crcs"]:
+                    bad_ranges += 1
+                continue
             rest = np.arange(n_gold, k)
             for i in rest[np.linspace(0, rest.size - 1, min(16, rest.size)).astype(np.int64)] if rest.size else []:
                 d = kvsep.splitmix64_bytes(int(plan.ln[i]), plan.seed, base + int(plan.off[i]))
                 mism += int(oracle.extend_addr(0, d.ctypes.data, d.size) != int(got[i]))
                 sampled += 1
-    return {"blocks_checked_vs_reference": checked, "blocks_sampled_vs_oracle": sampled, "mismatches": mism}
+    return {"blocks_total": total, "blocks_checked_vs_reference": checked,
+            "blocks_checked_vs_reference_digest": by_digest, "blocks_sampled_vs_oracle": sampled,
+            "every_block_checked": checked + by_digest == total, "mismatches": mism,
+            "mismatching_digest_ranges": bad_ranges}
 
 
 def live_pmc_traffic(args, timeout_s=240):
@@ -412,7 +440,10 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    if world > 1:
+    # Started by a launcher (torchrun, launch_ranks): a process group, RCCL with one rank per GPU -- also at one rank,
+    # so `torchrun --nproc-per-node 1 bench.py` runs the same RCCL init and collectives as eight ranks do
+    # (tests/test_gpu_rccl.py).  A plain `python bench.py` (N = 1) makes no process group and no collective.
+    if "WORLD_SIZE" in os.environ:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if os.environ.get("KVSEP_BENCH_SAME_DEVICE"):  # rehearsal: every rank on cuda:0, gloo for results
             local = 0
@@ -420,10 +451,10 @@ def main():
         else:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dd = dist if world > 1 else None
+    dd = dist if dist.is_initialized() else None
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    coll_dev = dev if world == 1 or dist.get_backend() == "nccl" else torch.device("cpu")
+    coll_dev = dev if dd is None or dist.get_backend() == "nccl" else torch.device("cpu")
 
     ctx = kvsep.Context(local)
     if args.piece_kib:
@@ -546,10 +577,7 @@ def main():
                        "outside the timed passes")
     elapsed = shard.max_over_ranks(elapsed, dd, coll_dev)
     total_useful = useful * npass
-    if dd:
-        t = torch.tensor([total_useful], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(t)
-        total_useful = int(t.item())
+    total_useful = int(shard.sum_over_ranks(total_useful, dd, coll_dev))
     ms_per_step = elapsed * 1e3 / args.steps
     value = total_useful * args.steps / GIB / elapsed
     kern_avg_ms = kern_ms / max(1, launches)
@@ -579,7 +607,7 @@ def main():
     if rank == 0:
         oracle = load_oracle()
         parity = check_results([Plan(args.config, world, r) for r in range(world)], results, oracle)
-        parity["all_blocks_match"] = parity["mismatches"] == 0
+        parity["all_blocks_match"] = parity["mismatches"] == 0 and parity["mismatching_digest_ranges"] == 0
         if not args.no_cpu and world == 1:
             aff = len(os.sched_getaffinity(0))
             most = args.cpu_threads or aff

@@ -24,6 +24,7 @@ int host_copy_parallel(kvsep_crc32c_ctx* c, char* const* dst, const char* const*
 // crc32c_host.cpp: kvsep_crc32c_batch_host whose gather also copies record i to tee[i] (one read of each payload).
 int batch_host_tee(kvsep_crc32c_ctx* c, const uint32_t* init, const char* const* ptr, const uint64_t* len,
                    uint32_t* out, uint64_t count, char* const* tee);
+void set_last_error(const char* msg);  // crc32c_host.cpp: the message kvsep_last_error() returns
 }  // namespace kvsep
 
 namespace {
@@ -45,6 +46,12 @@ constexpr uint64_t kVlogHeader = 8;       // db/log_format.h:40
 constexpr uint64_t kLogBlock = 32768;     // db/log_format.h:30
 constexpr uint64_t kLogHeader = 7;        // db/log_format.h:33
 constexpr uint64_t kSstTrailer = 5;       // table/format.h:81 kBlockTrailerSize
+
+// Every invalid-argument return posts its reason first, so kvsep_last_error() never carries a stale message.
+inline int einval(const char* why) {
+  kvsep::set_last_error(why);
+  return KVSEP_EINVAL;
+}
 
 }  // namespace
 
@@ -70,7 +77,7 @@ uint64_t kvsep_vlog_walk(const char* buf, uint64_t n, uint64_t* off, uint64_t* l
 
 int kvsep_vlog_verify_host(kvsep_crc32c_ctx* ctx, const char* buf, uint64_t n, uint64_t* nrecords, uint64_t* ngood,
                            uint64_t* good_bytes, uint64_t* drop_bytes) {
-  if (!ctx || (!buf && n)) return KVSEP_EINVAL;
+  if (!ctx || (!buf && n)) return einval("kvsep_vlog_verify_host: null argument");
   const uint64_t cnt = kvsep_vlog_walk(buf, n, nullptr, nullptr, nullptr, 0, nullptr);
   std::vector<uint64_t> off(cnt), len(cnt);
   std::vector<uint32_t> stored(cnt), crc(cnt);
@@ -90,14 +97,15 @@ int kvsep_vlog_verify_host(kvsep_crc32c_ctx* ctx, const char* buf, uint64_t n, u
 
 int kvsep_vlog_frame_host(kvsep_crc32c_ctx* ctx, const char* const* payload, const uint64_t* len, uint64_t count,
                           char* dst, uint64_t dst_cap, uint64_t* written) {
-  if (!ctx || (count && (!payload || !len))) return KVSEP_EINVAL;
+  if (!ctx || (count && (!payload || !len))) return einval("kvsep_vlog_frame_host: null argument");
   uint64_t need = 0;
   for (uint64_t i = 0; i < count; ++i) {
-    if (len[i] > 0xffffffffull) return KVSEP_EINVAL;  // db/value_log_writer.cc:48 (LE32 length)
+    if (len[i] > 0xffffffffull)  // db/value_log_writer.cc:48 (LE32 length)
+      return einval("kvsep_vlog_frame_host: payload longer than 2^32 - 1 bytes");
     need += kVlogHeader + len[i];
   }
   if (written) *written = need;
-  if (need > dst_cap || (need && !dst)) return KVSEP_EINVAL;
+  if (need > dst_cap || (need && !dst)) return einval("kvsep_vlog_frame_host: destination too small");
   // Checksums first, then the payload copy into the framed image as a pass of its own.  For ~1 MiB group-commit
   // payloads that measured faster than copying each payload into the image from the gather that stages it (the
   // tee that the log writer's <= 32 KiB fragments use): 36.5 vs 31.3 GiB/s, medians of three alternating runs.
@@ -144,10 +152,10 @@ uint64_t kvsep_log_walk(const char* buf, uint64_t n, uint64_t* off, uint64_t* le
 
 int kvsep_log_verify_host(kvsep_crc32c_ctx* ctx, const char* buf, uint64_t n, uint8_t* ok, uint64_t cap,
                           uint64_t* nrecords) {
-  if (!ctx || (!buf && n)) return KVSEP_EINVAL;
+  if (!ctx || (!buf && n)) return einval("kvsep_log_verify_host: null argument");
   const uint64_t cnt = kvsep_log_walk(buf, n, nullptr, nullptr, nullptr, nullptr, 0);
   if (nrecords) *nrecords = cnt;
-  if (cnt > cap || (cnt && !ok)) return KVSEP_EINVAL;
+  if (cnt > cap || (cnt && !ok)) return einval("kvsep_log_verify_host: verdict array too small");
   std::vector<uint64_t> off(cnt), len(cnt);
   std::vector<uint32_t> stored(cnt), crc(cnt);
   kvsep_log_walk(buf, n, off.data(), len.data(), stored.data(), nullptr, cnt);
@@ -161,7 +169,7 @@ int kvsep_log_verify_host(kvsep_crc32c_ctx* ctx, const char* buf, uint64_t n, ui
 
 int kvsep_log_frame_host(kvsep_crc32c_ctx* ctx, const char* const* payload, const uint64_t* len, uint64_t count,
                          uint64_t dest_length, char* dst, uint64_t dst_cap, uint64_t* written) {
-  if (!ctx || (count && (!payload || !len))) return KVSEP_EINVAL;
+  if (!ctx || (count && (!payload || !len))) return einval("kvsep_log_frame_host: null argument");
   struct Frag {
     const char* src;
     uint64_t len, at;  // payload bytes; offset of its header in dst
@@ -194,7 +202,7 @@ int kvsep_log_frame_host(kvsep_crc32c_ctx* ctx, const char* const* payload, cons
     } while (left > 0);
   }
   if (written) *written = p;
-  if (p > dst_cap || (p && !dst)) return KVSEP_EINVAL;
+  if (p > dst_cap || (p && !dst)) return einval("kvsep_log_frame_host: destination too small");
   const uint64_t nf = frags.size();
   std::vector<const char*> src(nf);
   std::vector<uint64_t> flen(nf);
@@ -230,7 +238,8 @@ int kvsep_log_frame_host(kvsep_crc32c_ctx* ctx, const char* const* payload, cons
 
 int kvsep_sst_trailers_host(kvsep_crc32c_ctx* ctx, const char* const* block, const uint64_t* len, const uint8_t* types,
                             uint32_t* masked_out, uint64_t count) {
-  if (!ctx || (count && (!block || !len || !types || !masked_out))) return KVSEP_EINVAL;
+  if (!ctx || (count && (!block || !len || !types || !masked_out)))
+    return einval("kvsep_sst_trailers_host: null argument");
   if (!count) return KVSEP_OK;
   // Value(block) for every block in one batched call through the pinned staging, then the trailer's one-byte
   // extension by the type and Mask on the host (table/table_builder.cc:222-225)
@@ -245,11 +254,12 @@ int kvsep_sst_trailers_host(kvsep_crc32c_ctx* ctx, const char* const* block, con
 
 int kvsep_sst_verify_host(kvsep_crc32c_ctx* ctx, const char* file, uint64_t n, const uint64_t* off, const uint64_t* len,
                           uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count) {
-  if (!ctx || (!file && n) || (count && (!off || !len || !out))) return KVSEP_EINVAL;
+  if (!ctx || (!file && n) || (count && (!off || !len || !out))) return einval("kvsep_sst_verify_host: null argument");
   std::vector<uint64_t> len1(count);
   for (uint64_t i = 0; i < count; ++i) {
     // the handle must leave room for the 5-byte trailer (table/format.cc:84-87: "truncated block read")
-    if (off[i] > n || len[i] > n - off[i] || n - off[i] - len[i] < kSstTrailer) return KVSEP_EINVAL;
+    if (off[i] > n || len[i] > n - off[i] || n - off[i] - len[i] < kSstTrailer)
+      return einval("kvsep_sst_verify_host: block handle (plus its 5-byte trailer) outside the file image");
     len1[i] = len[i] + 1;  // Value(data, n + 1): the block and its type byte (format.cc:102)
   }
   if (count) {

@@ -437,6 +437,8 @@ class Context:
         ptrs = (ctypes.c_void_p * max(k, 1))(*[x[0].value for x in keep])
         lens = np.array([x[1].nbytes for x in keep], dtype=np.uint64)
         t = np.ascontiguousarray(types, dtype=np.uint8)
+        if t.size != k:
+            raise ValueError("blocks and types must have the same length")
         out = np.zeros(max(k, 1), dtype=np.uint32)
         _check(lib().kvsep_sst_trailers_host(self._h, ptrs, lens.ctypes.data_as(ctypes.c_void_p),
                                              t.ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p), k),
@@ -466,6 +468,8 @@ class Context:
         p, keep = _buf(image)
         off = np.ascontiguousarray(off, dtype=np.uint64)
         length = np.ascontiguousarray(length, dtype=np.uint64)
+        if off.size != length.size:
+            raise ValueError("off and length must have the same length")
         k = off.size
         out = np.zeros(max(k, 1), dtype=np.uint32)
         fb, nb = ctypes.c_uint64(), ctypes.c_uint64()

@@ -13,6 +13,12 @@ from __future__ import annotations
 import numpy as np
 
 
+def _active(dist) -> bool:
+    """A collective runs whenever a process group is up -- also a one-rank group (so a one-rank RCCL communicator
+    runs the same all_gather / all_reduce code as eight ranks do: tests/test_gpu_rccl.py); no group, no collective."""
+    return dist is not None and dist.is_initialized()
+
+
 def stream_offset(rank: int, span: int) -> int:
     """Global stream position of rank `rank`'s first data byte."""
     return rank * span
@@ -48,7 +54,7 @@ def gather_results(crcs: np.ndarray, dist, device) -> list[np.ndarray]:
     import torch
 
     crcs = np.ascontiguousarray(crcs, dtype=np.uint32)
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+    if not _active(dist):
         return [crcs]
     world = dist.get_world_size()
     n = torch.tensor([crcs.size], dtype=torch.int64, device=device)
@@ -73,7 +79,7 @@ def crc_of_crcs(crcs: np.ndarray, extend_host) -> int:
 def max_over_ranks(value: float, dist, device) -> float:
     import torch
 
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+    if not _active(dist):
         return value
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -83,36 +89,18 @@ def max_over_ranks(value: float, dist, device) -> float:
 def min_over_ranks(value: float, dist, device) -> float:
     import torch
 
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+    if not _active(dist):
         return value
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return float(t.item())
 
 
-def gather_digests(digest: int, dist, device) -> list[int]:
-    """All-gather one 32-bit digest per rank (the only result traffic between GPUs)."""
+def sum_over_ranks(value: float, dist, device) -> float:
     import torch
 
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
-        return [digest]
-    t = torch.tensor([digest], dtype=torch.int64, device=device)
-    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
-    dist.all_gather(out, t)
-    return [int(x.item()) for x in out]
-
-
-def reduce_verify(nbad: int, first_bad: int, dist, device) -> tuple[int, int]:
-    """Verify mode across ranks: total mismatches and the lowest mismatching GLOBAL block index
-    (first_bad already offset by rank*count; UINT64_MAX-as-int64 == -1 means none)."""
-    import torch
-
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
-        return nbad, first_bad
-    big = np.iinfo(np.int64).max
-    n = torch.tensor([nbad], dtype=torch.int64, device=device)
-    f = torch.tensor([big if first_bad < 0 else first_bad], dtype=torch.int64, device=device)
-    dist.all_reduce(n, op=dist.ReduceOp.SUM)
-    dist.all_reduce(f, op=dist.ReduceOp.MIN)
-    fb = int(f.item())
-    return int(n.item()), (-1 if fb == big else fb)
+    if not _active(dist):
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())

@@ -56,6 +56,7 @@ int batch_host_tee(kvsep_crc32c_ctx* c, const uint32_t* init, const char* const*
     if (tee && tee[i] && len[i]) std::memcpy(tee[i], ptr[i], len[i]);
   return kvsep_crc32c_batch_host(c, init, ptr, len, out, count);
 }
+void set_last_error(const char*) {}
 }  // namespace kvsep
 
 int main() {

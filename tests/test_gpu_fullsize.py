@@ -1,8 +1,8 @@
 """GPU parity at BASELINE.json's full sizes, EVERY block against the reference (util/crc32c.cc compiled into
 oracle/_ref and run over the same synthetic streams by tests/golden/make_fullsize_golden.py):
 
-  config 2   65,536 x 4 KiB                                   256 MiB   tests/golden/full_cfg2.u32
-  config 3a  65,536 x 1 MiB                                   64 GiB    tests/golden/full_cfg3a.u32
+  config 2   65,536 x 4 KiB                                   256 MiB   tests/golden/full_cfg2.u32 (rank 0's part)
+  config 3a  65,536 x 1 MiB                                   64 GiB    tests/golden/full_cfg3a.u32 (rank 0's part)
   config 3b  65,536 x 1,048,609-B vlog records, odd offsets   64 GiB    slice 0 of full_cfg5.u32
   config 4   1,048,576 Zipf blocks, 32 B - 4 MiB              149.7 GiB tests/golden/full_cfg4.u32
   config 5   the 512 GiB vlog (524,288 records) as 8 distinct 64 GiB slices, each regenerated in HBM at its true
@@ -39,8 +39,8 @@ def u64(a):
 
 
 CONFIGS = {  # layout, seed, reference per-block CRCs
-    "2": (W.cfg2_layout, W.SEED, lambda: golden("full_cfg2.u32")),
-    "3a": (W.cfg3_layout, W.SEED + 1, lambda: golden("full_cfg3a.u32")),
+    "2": (W.cfg2_layout, W.SEED, lambda: golden("full_cfg2.u32")[:W.CFG2_BLOCKS]),  # rank 0 of the 8-rank files
+    "3a": (W.cfg3_layout, W.SEED + 1, lambda: golden("full_cfg3a.u32")[:W.CFG3_BLOCKS]),
     "3b": (lambda: W.cfg3_layout(vlog=True), W.SEED + 1, lambda: golden("full_cfg5.u32")[:W.CFG3_BLOCKS]),
     "4": (W.cfg4_layout, W.SEED + 2, lambda: golden("full_cfg4.u32")),
 }

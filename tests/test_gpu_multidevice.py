@@ -80,7 +80,7 @@ def test_group_vlog_scan_like_gc(group, oracle):
 def test_group_device_shards_vs_reference(group):
     """Device-resident shards of config 2 (the reference's full-batch CRCs): one shard per member."""
     off, ln = W.cfg2_layout()
-    ref = np.fromfile(os.path.join(GOLDEN, "full_cfg2.u32"), dtype="<u4")
+    ref = np.fromfile(os.path.join(GOLDEN, "full_cfg2.u32"), dtype="<u4")[:W.CFG2_BLOCKS]
     data = torch.empty(int(ln.sum()) + 64, dtype=torch.uint8, device=DEV)
     kvsep.fill_splitmix64(data.data_ptr(), int(ln.sum()), W.SEED, 0)
     b = kvsep.partition(ln, 2)
@@ -138,7 +138,7 @@ def test_group8_device_shards_index_base_vs_reference(group8):
     """All of config 2 (the reference's whole-batch CRCs) as eight device shards with index_base: results, and the
     global first_bad / nbad of stored words corrupted in members 2, 5 and 7."""
     off, ln = W.cfg2_layout()
-    ref = np.fromfile(os.path.join(GOLDEN, "full_cfg2.u32"), dtype="<u4")
+    ref = np.fromfile(os.path.join(GOLDEN, "full_cfg2.u32"), dtype="<u4")[:W.CFG2_BLOCKS]
     data = torch.empty(int(ln.sum()) + 64, dtype=torch.uint8, device=DEV)
     kvsep.fill_splitmix64(data.data_ptr(), int(ln.sum()), W.SEED, 0)
     b = kvsep.partition(ln, 8)
@@ -243,8 +243,8 @@ def test_two_ranks_config5_all_records_vs_reference():
 def test_two_ranks_config2_gathered_results():
     line = _torchrun_bench(2, "--config", "2", "--steps", "4", "--warmup", "1")
     p = line["parity"]
-    assert p["blocks_checked_vs_reference"] == 65536 and p["blocks_sampled_vs_oracle"] == 16
-    assert p["mismatches"] == 0 and len(line["digests"]) == 2
+    assert p["blocks_checked_vs_reference"] == 2 * 65536 and p["blocks_sampled_vs_oracle"] == 0
+    assert p["every_block_checked"] and p["mismatches"] == 0 and len(line["digests"]) == 2
 
 
 def test_bench_self_launch_two_ranks_config2():
@@ -261,4 +261,22 @@ def test_bench_self_launch_two_ranks_config2():
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["world_size"] == 2 and line["backend"] == "gloo", line
     p = line["parity"]
-    assert p["blocks_checked_vs_reference"] == 65536 and p["mismatches"] == 0, p
+    assert p["blocks_checked_vs_reference"] == 2 * 65536 and p["mismatches"] == 0, p
+
+
+def test_bench_self_launch_eight_ranks_config2_every_block():
+    """`python3 bench.py --gpus 8 --config 2` self-launched: eight ranks x 256 MiB, all on cuda:0
+    (KVSEP_BENCH_SAME_DEVICE, gloo for the results), and EVERY one of the 524,288 blocks of the 8-rank global batch is
+    checked against the reference's CRCs (tests/golden/full_cfg2.u32), none sampled."""
+    env = dict(os.environ, KVSEP_BENCH_SAME_DEVICE="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--config", "2", "--steps", "3", "--warmup",
+           "1", "--no-cpu", "--roundtrip-gib", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 8 and line["world_size"] == 8 and len(line["digests"]) == 8, line
+    p = line["parity"]
+    assert p["blocks_checked_vs_reference"] == 524288 and p["blocks_sampled_vs_oracle"] == 0, p
+    assert p["every_block_checked"] and p["mismatches"] == 0, p

@@ -206,3 +206,38 @@ def test_every_end_geometry(oracle, pool, kernel):
     got = run(ctx, d, off, ln, init=init)
     ctx.close()
     assert np.array_equal(got, oracle.batch(data, off, ln, init))
+
+
+@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted"])
+def test_verify_mismatch_on_deferred_block(oracle, pool, kernel):
+    """Verify form under an understated max_len: blocks longer than the hint leave their 8-block group and
+    are checksummed by the deferred walk, whose compare is verify_uniform over the wave-uniform stored word.  Mismatches
+    planted on deferred blocks (and one on an in-group block) must give the exact first_bad / nbad and CRCs."""
+    data, d = pool
+    rng = np.random.default_rng(4242)
+    count = 3000
+    ln = rng.integers(0, 2049, count).astype(np.uint64)
+    long_ix = rng.choice(count, 40, replace=False)
+    ln[long_ix] = rng.integers(2049, 40000, long_ix.size)  # over the 2048-B hint: deferred
+    off = rng.integers(0, data.size - 40001, count).astype(np.uint64)
+    init = rng.integers(0, 2**32, count, dtype=np.uint64).astype(np.uint32)
+    exp = oracle.batch(data, off, ln, init, threads=8)
+    deferred = sorted(int(i) for i in long_ix[:3])
+    short_bad = int(np.flatnonzero(ln <= 2048)[count // 2 % 100])
+    bad = sorted(set(deferred + [short_bad]))
+    ctx = kvsep.Context(0)
+    try:
+        ctx.set_kernel(kernel)
+        for planted in ([deferred[-1]], bad):  # a deferred block alone, then mixed with an in-group one
+            m = np.array([oracle.lib.oracle_crc32c_mask(int(c)) for c in exp], np.uint32)
+            m[planted] ^= 0x20
+            out = torch.zeros(count, dtype=torch.int32, device=DEV)
+            fb = torch.zeros(1, dtype=torch.int64, device=DEV)
+            nb = torch.zeros(1, dtype=torch.int64, device=DEV)
+            ctx.verify_device(d.data_ptr(), dev_u64(off), dev_u64(ln), dev_u32(m), out, fb, nb, init=dev_u32(init),
+                              total_bytes=int(ln.sum()), max_len=2048)
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), exp)
+            assert (fb.item(), nb.item()) == (min(planted), len(planted)), planted
+    finally:
+        ctx.close()

@@ -26,6 +26,26 @@ def _free_port():
     return p
 
 
+def gather_digests(digest: int, dist, device) -> list[int]:
+    """All-gather one 32-bit digest per rank."""
+    t = torch.tensor([digest], dtype=torch.int64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [int(x.item()) for x in out]
+
+
+def reduce_verify(nbad: int, first_bad: int, dist, device) -> tuple[int, int]:
+    """Verify mode across ranks: total mismatches and the lowest mismatching GLOBAL block index (first_bad already
+    offset by the rank's index base; -1 means none) -- the reduction kvsep_crc32c_group_verify_device does in-process."""
+    big = np.iinfo(np.int64).max
+    n = torch.tensor([nbad], dtype=torch.int64, device=device)
+    f = torch.tensor([big if first_bad < 0 else first_bad], dtype=torch.int64, device=device)
+    dist.all_reduce(n, op=dist.ReduceOp.SUM)
+    dist.all_reduce(f, op=dist.ReduceOp.MIN)
+    fb = int(f.item())
+    return int(n.item()), (-1 if fb == big else fb)
+
+
 def _worker(rank, world, port, q):
     sys.path.insert(0, os.path.join(ROOT, "kv-separate_amd"))
     import kvsep
@@ -39,7 +59,7 @@ def _worker(rank, world, port, q):
     ln = np.full(COUNT, LEN, dtype=np.uint64)
     data = splitmix64_bytes(SPAN + 16, 0xC0FFEE, shard.stream_offset(rank, SPAN))
     crcs = np.array([kvsep.extend_host(0, data[int(o):int(o + l)]) for o, l in zip(off, ln)], dtype=np.uint32)
-    digests = shard.gather_digests(shard.crc_of_crcs(crcs, kvsep.extend_host), dist, dev)
+    digests = gather_digests(shard.crc_of_crcs(crcs, kvsep.extend_host), dist, dev)
     elapsed = shard.max_over_ranks(0.5 + rank, dist, dev)
     assert shard.min_over_ranks(0.5 + rank, dist, dev) == 0.5
     # verify mode: rank 1 sees a corrupted record 7 (global index COUNT + 7)
@@ -48,7 +68,7 @@ def _worker(rank, world, port, q):
         expected[7] ^= 1
     bad = np.nonzero(np.array([kvsep.mask(int(c)) for c in crcs], np.uint32) != expected)[0]
     fb = int(bad[0]) + rank * COUNT if bad.size else -1
-    nbad, first = shard.reduce_verify(int(bad.size), fb, dist, dev)
+    nbad, first = reduce_verify(int(bad.size), fb, dist, dev)
     q.put((rank, digests, elapsed, nbad, first, crcs.tolist()))
     dist.destroy_process_group()
 
@@ -117,7 +137,7 @@ def _ragged_worker(rank, world, port, q):
     if rank == world - 1:
         stored[5] ^= 0x40
     bad = np.flatnonzero(np.array([kvsep.mask(int(c)) for c in crcs], np.uint32) != stored)
-    nbad, first = shard.reduce_verify(int(bad.size), ib + int(bad[0]) if bad.size else -1, dist, dev)
+    nbad, first = reduce_verify(int(bad.size), ib + int(bad[0]) if bad.size else -1, dist, dev)
     q.put((rank, [p.tolist() for p in parts], ib, int(ln.sum()), nbad, first))
     dist.destroy_process_group()
 

@@ -105,10 +105,11 @@ def _full(name):
 
 def test_fullsize_files_agree_with_the_small_fixtures(golden):
     c2, c5, c4, c3a = _full("full_cfg2.u32"), _full("full_cfg5.u32"), _full("full_cfg4.u32"), _full("full_cfg3a.u32")
-    assert (c2.size, c3a.size, c5.size, c4.size) == (65536, 65536, 8 * 65536, 1 << 20)
+    assert (c2.size, c3a.size, c5.size, c4.size) == (8 * 65536, 8 * 65536, 8 * 65536, 1 << 20)  # 8-rank batches
     g2 = golden["cfg2"]
     assert c2[:256].tolist() == g2["first"]
-    assert int(np.bitwise_xor.reduce(c2)) == g2["xor"] and int(c2.astype(np.uint64).sum()) == g2["sum"]
+    r0 = c2[:65536]  # rank 0's part is config 2 itself
+    assert int(np.bitwise_xor.reduce(r0)) == g2["xor"] and int(r0.astype(np.uint64).sum()) == g2["sum"]
     assert c5[:32].tolist() == golden["cfg3b"]["crc"]          # slice 0 of config 5 is config 3b
     assert c4[:512].tolist() == golden["cfg4"]["crc"]
 
@@ -126,8 +127,11 @@ def test_oracle_matches_fullsize_reference_samples(oracle):
     every slice, i.e. stream offsets up to 448 GiB)."""
     rng = np.random.default_rng(7)
     off, ln = W.cfg3_layout()
-    idx = rng.integers(0, off.size, 6)
-    assert _oracle_blocks(oracle, W.SEED + 1, 0, off, ln, idx) == _full("full_cfg3a.u32")[idx].tolist()
+    span = int(off[-1] + ln[-1])
+    c3a = _full("full_cfg3a.u32")
+    for r in (0, 3, 7):  # rank r's blocks: stream bytes r * span + off[i], entry r * 65,536 + i
+        idx = rng.integers(0, off.size, 2)
+        assert _oracle_blocks(oracle, W.SEED + 1, r * span, off, ln, idx) == c3a[r * off.size + idx].tolist(), r
     off, ln = W.cfg3_layout(vlog=True)
     span = int(off[-1] + ln[-1])
     c5 = _full("full_cfg5.u32")
@@ -138,5 +142,8 @@ def test_oracle_matches_fullsize_reference_samples(oracle):
     idx = np.concatenate([rng.integers(0, off.size, 24), [off.size - 1]])
     assert _oracle_blocks(oracle, W.SEED + 2, 0, off, ln, idx) == _full("full_cfg4.u32")[idx].tolist()
     off, ln = W.cfg2_layout()
-    idx = rng.integers(0, off.size, 64)
-    assert _oracle_blocks(oracle, W.SEED, 0, off, ln, idx) == _full("full_cfg2.u32")[idx].tolist()
+    span = int(off[-1] + ln[-1])
+    c2 = _full("full_cfg2.u32")
+    for r in range(8):
+        idx = rng.integers(0, off.size, 8)
+        assert _oracle_blocks(oracle, W.SEED, r * span, off, ln, idx) == c2[r * off.size + idx].tolist(), r
