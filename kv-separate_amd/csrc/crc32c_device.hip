@@ -90,17 +90,6 @@ struct PiecesArgs {
   const DevTables* tabs;
 };
 
-#ifdef KVSEP_STAMPS  // diagnostic build: per-wave cycle sums of the work-loop segments
-__device__ unsigned long long g_kvsep_stamps[8192 * 8];
-#define KVSEP_RSTAMP(v) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory")
-#define KVSEP_STAMP(v)                                                                     \
-  do {                                                                                     \
-    __builtin_amdgcn_sched_barrier(0);                                                     \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");             \
-    __builtin_amdgcn_sched_barrier(0);                                                     \
-  } while (0)
-#endif
-
 // Descriptor reads through the constant address space: wave-uniform indices then lower to scalar
 // s_load (lgkmcnt), so fetching the next item's descriptors never drains the vmcnt of in-flight
 // payload loads.  Descriptors are read-only for the whole launch.
@@ -461,6 +450,8 @@ __device__ __forceinline__ uint32_t ld32(const uint32_t* p) {
   return *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(reinterpret_cast<uintptr_t>(p));
 }
 
+#include "crc32c_hooks.inc"  // diagnostic hook points: empty in the shipped library
+
 // LDS image of a CRC workgroup: the replicated fold table `rep` (4 byte-tables) at [0, 128 KiB), then the
 // small tables (Z_4, the tree tables, the byte table) as one contiguous run.
 struct NoMid {
@@ -599,10 +590,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   const uint32_t tid = threadIdx.x;
-#ifdef KVSEP_STAMPS  // diagnostic build (tools/stamp_probe.hip): per-wave realtime (100 MHz) budget, see the end
-  unsigned long long r0, r1;
-  KVSEP_RSTAMP(r0);
-#endif
+  KVSEP_WSTAMP_ENTRY();  // stamp hooks (crc32c_hooks.inc): empty in the shipped library
   const uint32_t lane = tid & 63u;
   uint32_t vz;  // 0, opaque to the uniformity analysis (see stage())
   asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
@@ -739,32 +727,14 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   // for ALL of B's loads (vmcnt(0)) and would put a full HBM latency back on every item.
   auto step = [&](uint64_t g, uint64_t end, Item& ia, Staged<kG>& A, Item& ib, Staged<kG>& B) {
     const bool hn = g + 1 < end;
-#ifdef KVSEP_STAMPS  // diagnostic build only (kv-separate_amd/tools/stamp_probe.hip)
-    unsigned long long t0;
-    KVSEP_RSTAMP(t0);
-#endif
+    KVSEP_WSTAMP_ITEM_BEGIN();
     // The next item's HBM loads overlap the end of this item's compute (finish() stages them late, see
     // there).  The take is unconditional (the last item re-stages itself): on a path without it, this item's loads would be the most recent ones and the
     // compiler's counted wait (which merges both paths) would drain everything, vmcnt(0), on every item.
     emit(ia, finish<kG, kNT, kAbl, kAlign>(lds, A, ia.reg0, lane, lc0, lc1, [&]() {
            if (kAhead) take(hn ? g + 1 : g, ib, B);
          }));
-#ifdef KVSEP_STAMPS
-    {
-      // per wave: [0] / [1] ticks in whole-block items / in pieces of split blocks, [2] / [3] their counts, [7] the
-      // last item (bit 63 whole block, bit 62 a block's first piece, bits 40-61 its ticks, bits 0-39 its index)
-      unsigned long long t1;
-      KVSEP_RSTAMP(t1);
-      if (lane == 0) {
-        unsigned long long* st = &g_kvsep_stamps[(uint64_t(blockIdx.x) * kWavesPerWg + wave) * 8];
-        const unsigned long long d = t1 - t0;
-        st[ia.only ? 0 : 1] += d;
-        st[ia.only ? 2 : 3] += 1;
-        st[7] = (ia.only ? 1ull << 63 : 0ull) | (ia.reg0 != 0 ? 1ull << 62 : 0ull) | ((d & 0x3fffffull) << 40) |
-                (ia.g & 0xffffffffffull);
-      }
-    }
-#endif
+    KVSEP_WSTAMP_ITEM_END(ia);
     if (!kAhead && hn) take(g + 1, ib, B);
     return hn;
   };
@@ -773,10 +743,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   Staged<kG> S, T;
   fill_lds<kThreads>(lds, &a.tabs->z1024[0][0], a.tabs, tid);
   __syncthreads();
-#ifdef KVSEP_STAMPS
-  unsigned long long rf;
-  KVSEP_RSTAMP(rf);
-#endif
+  KVSEP_WSTAMP_FILLED();
   while (grab()) {
     for (uint64_t ws = lo; ws < hi; ws += 64) {
       fill(ws, hi);
@@ -788,15 +755,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
       }
     }
   }
-#ifdef KVSEP_STAMPS
-  KVSEP_RSTAMP(r1);
-  if (lane == 0) {  // [4] entry, [5] LDS fill done, [6] exit (realtime)
-    unsigned long long* st = &g_kvsep_stamps[(uint64_t(blockIdx.x) * kWavesPerWg + wave) * 8];
-    st[4] = r0;
-    st[5] = rf;
-    st[6] = r1;
-  }
-#endif
+  KVSEP_WSTAMP_EXIT();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1168,21 +1127,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
 
   NItem cur, nxt;
   NStaged<kG> S, T;
-#ifdef KVSEP_STAMPS  // diagnostic build (tools/stamp_probe.hip): realtime (100 MHz) at entry, after the fill, after
-                     // each group (up to 5), and at exit, per wave
-  unsigned long long* nst = &g_kvsep_stamps[(uint64_t(blockIdx.x) * kWavesPerWg + wave) * 8];
-  unsigned long long tnow;
-  int nsteps = 0;
-  KVSEP_RSTAMP(tnow);
-  if (lane == 0) nst[0] = tnow;
-#define KVSEP_NSTAMP(k)                  \
-  do {                                   \
-    KVSEP_RSTAMP(tnow);                  \
-    if (lane == 0) nst[k] = tnow;        \
-  } while (0)
-#else
-#define KVSEP_NSTAMP(k) do {} while (0)
-#endif
+  KVSEP_NSTAMP_ENTRY();  // stamp hooks (crc32c_hooks.inc): empty in the shipped library
   // The first group's descriptors are fetched during the LDS fill.  Staging its rows before the fill as well
   // measured 4-7 % slower on 256 MiB-1 GiB batches of 4 KiB blocks: the fill then waits behind them.
   if (kOverlap) {
@@ -1208,11 +1153,6 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     }
   }
   KVSEP_NSTAMP(1);
-#ifdef KVSEP_STAMPS
-#define KVSEP_NSTEP() do { if (nsteps < 5) KVSEP_NSTAMP(2 + nsteps); ++nsteps; } while (0)
-#else
-#define KVSEP_NSTEP() do {} while (0)
-#endif
   if (lo < hi) {
     for (uint64_t g = lo;; g += 2 * kPerGroup) {
       const bool more = step(g, cur, S, nxt, T);
@@ -1224,8 +1164,6 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     }
   }
   KVSEP_NSTAMP(7);
-#undef KVSEP_NSTEP
-#undef KVSEP_NSTAMP
   if (deferred) narrow_deferred<kG, kNT, kAlignN, Lay, kVerify>(a, lds, lo, hi, dummy);
 }
 
@@ -1381,39 +1319,9 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesAr
       if (kVerify) verify_wave(a, lane, j == kNarrowLanes - 1 && ia.live, ia.w, ia.src, ~reg, ex);  // before the store
       if (j == kNarrowLanes - 1 && ia.live) {
         emit_block(a, ia.w + ia.src, ~reg);
-#ifdef KVSEP_DIAG
-        const uint64_t b = ia.w + ia.src;
-        if ((kVIn == 1 || kVIn == 3 || kVIn == 4) && a.expect && mask_crc(~reg) != a.expect[b]) {
-          atomicMin(a.first_bad, (unsigned long long)b);
-          atomicAdd(a.nbad, 1ull);
-        }
-        if (kVIn == 5 && a.expect && mask_crc(~reg) != a.expect[b]) *a.first_bad = b;  // plain store
-        if (kVIn == 2 && a.expect) {
-          uint32_t z = 0;
-          asm volatile("" : "+v"(z));
-          a.out[b] = ~reg ^ (a.expect[b] & z);
-        }
-#endif
+        diag_sorted_emit<kVIn>(a, ia.w + ia.src, reg);  // diag build only (crc32c_hooks.inc)
       }
-#ifdef KVSEP_DIAG
-      if (kVIn == 3) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // wait states after the join
-      if (kVIn == 4) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      if (kVIn == 6 && a.expect) {  // compare with no divergent region around it: load, compare, ballot in full EXEC
-        const bool mine = j == kNarrowLanes - 1 && ia.live;
-        const uint64_t b = mine ? ia.w + ia.src : 0;
-        const bool bad = mine && mask_crc(~reg) != a.expect[b];
-        const uint64_t m = __builtin_amdgcn_ballot_w64(bad);
-        if (m) {  // wave-uniform
-          const uint32_t src = uint32_t(__builtin_ctzll(m));
-          const uint64_t fb = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(b >> 32)), int(src)))) << 32) |
-                              uint32_t(__builtin_amdgcn_readlane(int(uint32_t(b)), int(src)));
-          if (lane == 0) {
-            atomicMin(a.first_bad, (unsigned long long)fb);
-            atomicAdd(a.nbad, (unsigned long long)__builtin_popcountll(m));
-          }
-        }
-      }
-#endif
+      diag_sorted_join<kVIn>(a, j == kNarrowLanes - 1 && ia.live, ia.w, ia.src, reg, lane);
       if (kDrain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (here) {
         ++k;
@@ -1590,10 +1498,6 @@ __global__ void __launch_bounds__(512) stream_read_kernel(uintptr_t src, uint64_
 
 }  // namespace kvsep
 
-#ifdef KVSEP_DIAG
-#include "crc32c_diag.inc"  // the tools build's A/B variants (never in the shipped library)
-#endif
-
 // ================================================================================================
 // host side
 using namespace kvsep;
@@ -1618,6 +1522,10 @@ struct kvsep_crc32c_ctx {
   HostStaging staging;
   std::mutex mu;
 };
+
+// The KVSEP_DIAG tools build's launch variants and host hooks; in the shipped library the hooks are constant-false
+// inline functions (no variant is reachable, no environment variable is read).
+#include "crc32c_diag.inc"
 
 namespace {
 thread_local std::string g_last_error;
@@ -1759,10 +1667,8 @@ bool use_narrow(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t max_len) {
   if (max_len == 0 || max_len > 2 * kNarrowMax) return false;
   if (c->kernel == 1) return false;
   if (c->kernel >= 2) return true;
-#ifdef KVSEP_DIAG
-  if (!c->narrow) return false;
-  if (c->narrow >= 2) return true;
-#endif
+  const int d = diag_use_narrow(c);  // KVSEP_DIAG build only: -1 (no override) in the shipped library
+  if (d >= 0) return d != 0;
   const uint64_t cus = uint64_t(c->num_cus);
   return (max_len <= 8 * 1024 && count >= 32 * cus) || (max_len <= 16 * 1024 && count >= 64 * cus) ||
          (max_len <= kNarrowMax && count >= 128 * cus);
@@ -1807,10 +1713,7 @@ void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs
     crc32c_pieces_kernel<P, D, 4, true, true, 0, T, true, true><<<grid, T, 0, s>>>(a);
     return;
   }
-#ifdef KVSEP_DIAG
-  if (diag_launch_pieces<P, D>(variant, grid, s, a)) return;
-#endif
-  (void)variant;
+  if (diag_launch_pieces<P, D>(variant, grid, s, a)) return;  // KVSEP_DIAG build only
   crc32c_pieces_kernel<P, D, 4, true, true, 0, T><<<grid, T, 0, s>>>(a);
 }
 
@@ -1930,12 +1833,7 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
   }
   if (!planned && use_narrow(c, count, max_len)) {
     int nv = narrow_form(c, count, total_bytes, max_len);
-#ifdef KVSEP_DIAG
-    // diag narrow variants: 2: always 8 waves; 3: 12 waves; 4 / 5: 8-row groups at 8 / 12 waves; 6: always 16
-    // waves; 7: as 1; 9: 8 waves, fill overlapped with the first loads; 20 / 21 / 22: sorted windows at 16 / 8 / 12
-    // waves; 12, 14, 16-19: see the cases below
-    if (c->narrow != 1 && c->narrow != 7 && c->kernel < 3) nv = c->narrow;
-#endif
+    nv = diag_narrow_form(c, nv);  // KVSEP_DIAG build only
     a.hint = max_len;
     if (expect && (nv == 6 || nv == 9 || nv == 20)) {  // the verify form of the shipped narrow forms
       switch (nv) {
@@ -1944,11 +1842,9 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
         default: crc32c_narrow_kernel<4, true, 1024, false, 0, true, LdsFull, true><<<grid, 1024, 0, s>>>(a); break;
       }
     } else {
-    // diag variants 24-29 run their own in-kernel compare; every other diag variant gets verify_finish_kernel
-    fused = !expect || (nv >= 24 && nv <= 29);
-#ifdef KVSEP_DIAG
-    if (!diag_launch_narrow(nv, grid, s, a, count))
-#endif
+    // diag variants that run their own in-kernel compare; every other diag variant gets verify_finish_kernel
+    fused = !expect || diag_self_compare(nv);
+    if (!diag_launch_narrow(nv, grid, s, a, count))  // KVSEP_DIAG build only
     switch (nv) {
       case 9: crc32c_narrow_kernel<4, true, 512, true><<<grid, 512, 0, s>>>(a); break;
       case 20: crc32c_narrow_sorted_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
@@ -2026,11 +1922,7 @@ int kvsep_crc32c_ctx_create(int device, kvsep_crc32c_ctx** out) {
   auto* c = new kvsep_crc32c_ctx();
   c->device = device;
   c->num_cus = prop.multiProcessorCount;
-#ifdef KVSEP_DIAG  // tools build only: no environment variable reaches the shipped library's kernel choice
-  if (const char* v = std::getenv("KVSEP_CRC_VARIANT")) c->variant = std::atoi(v);
-  if (const char* v = std::getenv("KVSEP_NARROW")) c->narrow = std::atoi(v);
-  if (const char* v = std::getenv("KVSEP_CRC_STATIC_RR")) c->static_contig = std::atoi(v) ? 0 : 1;
-#endif
+  diag_env(c);  // tools build only: no environment variable reaches the shipped library's kernel choice
   int rc = upload_tables(c);
   if (rc) {
     delete c;
@@ -2224,15 +2116,7 @@ int kvsep_stream_read_device(kvsep_crc32c_ctx* c, void* stream, const void* src,
     e1 = take_event(c);
     if (e0 && e1) KVSEP_HIP(hipEventRecord(e0, s));
   }
-#ifdef KVSEP_DIAG  // KVSEP_CRC_VARIANT 31-34: the read patterns with the fold chain (stream_fold_kernel)
-  if (c->variant >= 31 && c->variant <= 34) {
-    const uintptr_t sp = reinterpret_cast<uintptr_t>(src);
-    if (c->variant == 31) stream_fold_kernel<true, 8><<<unsigned(c->num_cus), 512, 0, s>>>(sp, n16, sink, c->d_tabs);
-    if (c->variant == 32) stream_fold_kernel<true, 4><<<unsigned(c->num_cus), 512, 0, s>>>(sp, n16, sink, c->d_tabs);
-    if (c->variant == 33) stream_fold_kernel<false, 8><<<unsigned(c->num_cus), 512, 0, s>>>(sp, n16, sink, c->d_tabs);
-    if (c->variant == 34) stream_fold_kernel<false, 4><<<unsigned(c->num_cus), 512, 0, s>>>(sp, n16, sink, c->d_tabs);
-  } else
-#endif
+  if (!diag_stream_read(c, s, reinterpret_cast<uintptr_t>(src), n16, sink))  // KVSEP_DIAG build only
   stream_read_kernel<<<unsigned(c->num_cus), 512, 0, s>>>(reinterpret_cast<uintptr_t>(src), n16, sink);
   KVSEP_HIP(hipGetLastError());
   if (c->timing && e0 && e1) {
