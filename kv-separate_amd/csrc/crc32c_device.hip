@@ -82,12 +82,18 @@ struct PiecesArgs {
                                     // 0: adaptive, clamp(total / (64 * nwaves), 4, 32)
   uint32_t guided_cap;              // dynamic schedule: at most this many items per grab (0: no cap)
   uint64_t hint;                    // narrow kernel: the caller's max_len hint; longer blocks are deferred (exact)
-  // verify form (kVerify kernels): Mask(crc of block b) must equal expect[b]; mismatches post the lowest block index
-  // (atomicMin) and their number (atomicAdd) -- the check of db/value_log_reader.cc:109-122 / table/format.cc:99-106
+  // verify form (kVerify kernels): Mask(crc of block b) must equal expect[b] -- the check of
+  // db/value_log_reader.cc:109-122 / table/format.cc:99-106.  The caller's result words first_bad (lowest mismatching
+  // block, ~0 if none) and nbad are written once, by the last workgroup of the publishing kernel (verify_publish).
   const uint32_t* expect;
   unsigned long long* first_bad;
   unsigned long long* nbad;
   const DevTables* tabs;
+  // The context's accumulator words, kept in their reset state between calls: vacc[0] = lowest mismatching block
+  // (~0: none), vacc[1] = (workgroups arrived << 40) | mismatches.  Mismatches post there (atomicMin / atomicAdd); the
+  // last workgroup to arrive copies them to first_bad / nbad and resets them, so a verify call needs no init launch.
+  unsigned long long* vacc;
+  uint32_t publish;  // the pieces kernel publishes (an unsplit batch) or leaves it to the combine kernel (a split one)
 };
 
 // Descriptor reads through the constant address space: wave-uniform indices then lower to scalar
@@ -417,8 +423,9 @@ __device__ __forceinline__ void emit_block(const PiecesArgs& a, uint64_t b, uint
 // whole wave (full EXEC) right after a group's emit: lanes with `mine` hold block b's crc and the stored word `ex`
 // they loaded before the next group's staging (so waiting for it never drains those loads).  The compare itself is
 // branch-free; the wave ballots the mismatches and only a mismatch enters a wave-uniform branch, where one lane posts
-// the wave's lowest mismatching index and the count.  A per-lane branch on the compare nested inside the emit's
-// divergent branch is what made the round-1 sorted-window kernel miscompute (diag variants 24-29).
+// the wave's lowest mismatching index and the count to the accumulator words (fenced at the end of the kernel, before
+// the workgroup arrives: verify_publish).  A per-lane branch on the compare nested
+// inside the emit's divergent branch is what made the round-1 sorted-window kernel miscompute.
 // The lane's block is base + idx (base wave-uniform): one VGPR for the index, not a 64-bit pair.
 __device__ __forceinline__ void verify_wave(const PiecesArgs& a, uint32_t lane, bool mine, uint64_t base, uint32_t idx,
                                             uint32_t crc, uint32_t ex) {
@@ -430,8 +437,8 @@ __device__ __forceinline__ void verify_wave(const PiecesArgs& a, uint32_t lane, 
       best = il < best ? il : best;
     }
     if (lane == 0) {
-      atomicMin(a.first_bad, (unsigned long long)(base + best));
-      atomicAdd(a.nbad, (unsigned long long)__builtin_popcountll(m));
+      atomicMin(a.vacc, (unsigned long long)(base + best));
+      atomicAdd(a.vacc + 1, (unsigned long long)__builtin_popcountll(m));
     }
   }
 }
@@ -439,9 +446,38 @@ __device__ __forceinline__ void verify_wave(const PiecesArgs& a, uint32_t lane, 
 // One block checked by a whole wave whose crc and stored word are wave-uniform (the wide kernel, the deferred walk).
 __device__ __forceinline__ void verify_uniform(const PiecesArgs& a, uint32_t lane, uint64_t b, uint32_t crc,
                                                uint32_t ex) {
-  if (mask_crc(crc) != ex && lane == 0) {
-    atomicMin(a.first_bad, (unsigned long long)b);
-    atomicAdd(a.nbad, 1ull);
+  if (__builtin_amdgcn_ballot_w64(mask_crc(crc) != ex)) {  // wave-uniform
+    if (lane == 0) {
+      atomicMin(a.vacc, (unsigned long long)b);
+      atomicAdd(a.vacc + 1, 1ull);
+    }
+  }
+}
+
+// The end of a publishing verify kernel, every workgroup: once its waves are done and have fenced their posts, wave 0
+// arrives on vacc[1] with one returning atomic; the last workgroup to arrive copies the verdict to
+// the caller's first_bad / nbad and puts the accumulators back in their reset state (~0, 0) for the next call.  The
+// mismatch count travels in the arrival word, so a clean batch costs the last workgroup one atomic round trip;
+// vacc[0] is read (and reset) only when something mismatched.  This replaces a separate init launch per call.
+// `wave`: the wave's index in the workgroup (wave-uniform, an SGPR); the lane is recomputed here (v_mbcnt) rather than
+// kept live from the kernel's start: at the 16-wave kernels' 128-VGPR cap one more long-lived VGPR spills.
+__device__ __forceinline__ void verify_publish(const PiecesArgs& a, uint32_t wave) {
+  __threadfence();  // this wave's posts (if any) are performed before the workgroup arrives
+  __syncthreads();
+  if (wave == 0) {
+    uint32_t lane;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+    unsigned long long old = 0;
+    if (lane == 0) old = atomicAdd(a.vacc + 1, 1ull << 40);
+    old = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(old >> 32)), 0))) << 32) |
+          uint32_t(__builtin_amdgcn_readlane(int(uint32_t(old)), 0));
+    if ((old >> 40) + 1 == gridDim.x && lane == 0) {  // the last workgroup
+      const unsigned long long nb = old & ((1ull << 40) - 1);
+      atomicExch(a.vacc + 1, 0ull);  // first, so the wait for the swap's result below is a plain vmcnt(0)
+      const unsigned long long fb = nb ? atomicExch(a.vacc, ~0ull) : ~0ull;
+      *a.first_bad = fb;
+      *a.nbad = nb;
+    }
   }
 }
 
@@ -756,6 +792,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
     }
   }
   KVSEP_WSTAMP_EXIT();
+  if (kVerify && a.publish) verify_publish(a, wave);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1165,6 +1202,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   }
   KVSEP_NSTAMP(7);
   if (deferred) narrow_deferred<kG, kNT, kAlignN, Lay, kVerify>(a, lds, lo, hi, dummy);
+  if (kVerify) verify_publish(a, wave);
 }
 
 // Bitonic sort of one (key, idx) pair per lane over the wavefront, ascending by key (ties by idx, so the two
@@ -1342,6 +1380,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesAr
     }
   }
   if (deferred) narrow_deferred<kG, kNT, true, LdsFull, kVerify>(a, lds, lo, hi, dummy);
+  if (kVerify) verify_publish(a, wave);
 }
 
 // One thread per block: Horner over the block's pieces, R <- Z_piece(R) ^ R_piece.  kVerify: also the verify form's
@@ -1366,7 +1405,10 @@ __global__ void __launch_bounds__(256) crc32c_combine_kernel(PiecesArgs a) {
     crc = ~acc;
     emit_block(a, b, crc);
   }
-  if (kVerify) verify_wave(a, threadIdx.x & 63u, mine, uint64_t(blockIdx.x) * 256, threadIdx.x, crc, ld32(a.expect + bb));
+  if (kVerify) {
+    verify_wave(a, threadIdx.x & 63u, mine, uint64_t(blockIdx.x) * 256, threadIdx.x, crc, ld32(a.expect + bb));
+    verify_publish(a, threadIdx.x >> 6);  // the split blocks' verdict: after the CRC kernel's whole-block posts
+  }
 }
 
 __global__ void crc32c_plan_count_kernel(const uint64_t* len, uint64_t count, uint64_t piece_bytes,
@@ -1394,14 +1436,6 @@ __global__ void __launch_bounds__(256) verify_finish_kernel(const uint32_t* out,
   if (lane == uint32_t(__builtin_ctzll(m))) {  // the wave's first bad block is its lowest bad index
     atomicMin(first_bad, (unsigned long long)b);
     atomicAdd(nbad, (unsigned long long)__builtin_popcountll(m));
-  }
-}
-
-// The verify form's result words before the CRC kernels post to them: first_bad = UINT64_MAX, nbad = 0.
-__global__ void __launch_bounds__(64) verify_init_kernel(unsigned long long* first_bad, unsigned long long* nbad) {
-  if (threadIdx.x == 0) {
-    *first_bad = ~0ull;
-    *nbad = 0;
   }
 }
 
@@ -1591,6 +1625,17 @@ int release(Scratch& sc, hipStream_t s) {
   return KVSEP_OK;
 }
 
+// The verify form's device words (32 B, allocated once per scratch, before any capture -- kvsep_crc32c_reserve does it):
+// [0] / [1] the result words of a call whose caller passes none, [2] / [3] the accumulators the kernels post to and
+// reset (PiecesArgs::vacc), which must start in their reset state: ~0 (no mismatch) and 0 (nothing arrived, none bad).
+int ensure_verify(Scratch& sc) {
+  if (sc.d_verify) return KVSEP_OK;
+  const unsigned long long init[4] = {~0ull, 0ull, ~0ull, 0ull};
+  KVSEP_HIP(hipMalloc(&sc.d_verify, sizeof init));
+  KVSEP_HIP(hipMemcpy(sc.d_verify, init, sizeof init, hipMemcpyHostToDevice));
+  return KVSEP_OK;
+}
+
 // SST verify scratch (len + 1 and the stored trailer words per block).
 int ensure_sst(Scratch& sc, uint64_t count) {
   if (count <= sc.cap_sst) return KVSEP_OK;
@@ -1775,19 +1820,22 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
   a.piece_bytes = planned ? piece_for(c, total_bytes, &a.zpiece) : c->piece_bytes;
   a.tabs = c->d_tabs;
   if (expect) {
+    int rc = ensure_verify(sc);
+    if (rc) return rc;
     if (!first_bad || !nbad) {
-      if (!sc.d_verify) KVSEP_HIP(hipMalloc(&sc.d_verify, 16));
       first_bad = reinterpret_cast<uint64_t*>(sc.d_verify);
       nbad = reinterpret_cast<uint64_t*>(sc.d_verify + 1);
     }
-    // one tiny launch for both words (two memset nodes cost two launches of the graph / stream)
-    verify_init_kernel<<<1, 64, 0, s>>>(reinterpret_cast<unsigned long long*>(first_bad),
-                                        reinterpret_cast<unsigned long long*>(nbad));
-    KVSEP_HIP(hipGetLastError());
+    a.vacc = sc.d_verify + 2;  // the accumulators, in their reset state: the kernels publish the verdict (no init)
+    if (count == 0) {          // nothing to check, no kernel: the verdict is "none" (first_bad = ~0, nbad = 0)
+      KVSEP_HIP(hipMemsetAsync(first_bad, 0xff, 8, s));
+      KVSEP_HIP(hipMemsetAsync(nbad, 0, 8, s));
+    }
   }
   a.expect = expect;
   a.first_bad = reinterpret_cast<unsigned long long*>(first_bad);
   a.nbad = reinterpret_cast<unsigned long long*>(nbad);
+  a.publish = planned ? 0u : 1u;  // a split batch's verdict is published by the combine kernel
   // The verify form's compare runs inside the CRC kernels (and the combine kernel for split blocks): `fused`.  Only
   // the A/B variants of the KVSEP_DIAG tools build fall back to the separate verify_finish_kernel pass.
   bool fused = true;
@@ -1842,7 +1890,12 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
         default: crc32c_narrow_kernel<4, true, 1024, false, 0, true, LdsFull, true><<<grid, 1024, 0, s>>>(a); break;
       }
     } else {
-    // diag variants that run their own in-kernel compare; every other diag variant gets verify_finish_kernel
+    // KVSEP_DIAG variants only (the shipped forms are 6, 9 and 20): they post to the caller's words directly, from
+    // their own in-kernel compare or from verify_finish_kernel, so those words are set first
+    if (expect) {
+      KVSEP_HIP(hipMemsetAsync(first_bad, 0xff, 8, s));
+      KVSEP_HIP(hipMemsetAsync(nbad, 0, 8, s));
+    }
     fused = !expect || diag_self_compare(nv);
     if (!diag_launch_narrow(nv, grid, s, a, count))  // KVSEP_DIAG build only
     switch (nv) {
@@ -1979,7 +2032,8 @@ int kvsep_crc32c_reserve(kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_byt
   KVSEP_HIP(dg.err);
   // everything a later call could allocate, so that the call can be captured into a hipGraph
   if (!c->sc.d_counter) KVSEP_HIP(hipMalloc(&c->sc.d_counter, 16));
-  if (!c->sc.d_verify) KVSEP_HIP(hipMalloc(&c->sc.d_verify, 16));
+  int vr = ensure_verify(c->sc);
+  if (vr) return vr;
   if (!c->sc.last_use) KVSEP_HIP(hipEventCreateWithFlags(&c->sc.last_use, hipEventDisableTiming));
   int rc = ensure_sst(c->sc, count);
   if (rc) return rc;

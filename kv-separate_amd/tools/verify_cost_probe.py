@@ -4,7 +4,8 @@
 For each config the same device-resident batch is checksummed K times by kvsep_crc32c_batch_device and K times by
 kvsep_crc32c_verify_device (correct stored words, so nbad = 0), each as ONE hipGraph of K back-to-back calls timed with
 a HIP event pair on the replay stream, interleaved over several rounds in one process; the median per-call time of each
-form is reported (whole call: the verify form adds one tiny init launch for its two result words), and the CRC kernel
+form is reported (whole call: since round 4 the verify form has no init launch -- the last workgroup publishes the
+verdict and resets the context's accumulators), and the CRC kernel
 alone (the library's event pair around it, eager launches).  Every verify call's results are checked (out == the batch form's, nbad == 0), and a last verify call
 with three planted bad words must report them.  Configs: 2 (65,536 x 4 KiB: the narrow kernel), 3b (65,536 vlog records
 of 1,048,609 B: the wide kernel + combine), 4s (config 4's blocks <= 32 KiB: the sorted-window kernel).

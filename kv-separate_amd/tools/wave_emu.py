@@ -375,8 +375,8 @@ class Workgroup:
     def exec_insn(self, w, k, op, o):
         act = w.active()
         # ---------------- scalar control
-        if op in ('s_waitcnt', 's_nop', 's_setprio', 's_sleep') or op.startswith('sched_'):
-            return
+        if op in ('s_waitcnt', 's_nop', 's_setprio', 's_sleep', 'buffer_wbl2', 'buffer_inv') or op.startswith('sched_'):
+            return  # every memory op completes before the next instruction: waits and cache maintenance are no-ops
         if op == 's_endpgm':
             w.done = True
             return
@@ -856,6 +856,10 @@ class Workgroup:
             a, sh, b = V(o[1]), V(o[2]) & u(31), V(o[3])
             w.vset(o[0], (a << sh) | b)
             return
+        if base == 'v_lshl_add_u32':
+            a, sh, b = V(o[1]), V(o[2]) & u(31), V(o[3])
+            w.vset(o[0], ((a << sh) + b) & u(M32))
+            return
         if base == 'v_alignbit_b32':
             a, b, sh = V(o[1]).astype(np.uint64), V(o[2]).astype(np.uint64), (V(o[3]) & u(31)).astype(np.uint64)
             w.vset(o[0], (((a << np.uint64(32)) | b) >> sh) & np.uint64(M32))
@@ -945,22 +949,23 @@ class Workgroup:
 
 
 # ------------------------------------------------------------------------------------------------------------------
-# PiecesArgs (csrc/crc32c_device.hip) field offsets; the hidden arguments follow the 160-byte struct
+# PiecesArgs (csrc/crc32c_device.hip) field offsets; the hidden arguments follow the 176-byte struct
 PIECES_ARGS = {"base": 0, "off": 8, "len": 16, "init": 24, "out": 32, "count": 40, "pstart": 48, "pblk": 56,
                "partial": 64, "work_counter": 72, "piece_bytes": 80, "zpiece": 88, "max_pieces": 96,
                "static_contig": (104, "<I"), "guided_div": (108, "<I"), "guided_cap": (112, "<I"), "hint": 120,
-               "expect": 128, "first_bad": 136, "nbad": 144, "tabs": 152}
+               "expect": 128, "first_bad": 136, "nbad": 144, "tabs": 152, "vacc": 160, "publish": (168, "<I")}
+ARGS_BYTES = 176
 
 
 def pieces_kernarg(fields: dict, grid: int, threads: int) -> bytes:
-    ka = bytearray(416)
+    ka = bytearray(ARGS_BYTES + 256)
     for k, v in fields.items():
         spec = PIECES_ARGS[k]
         o, fmt = spec if isinstance(spec, tuple) else (spec, "<Q")
         struct.pack_into(fmt, ka, o, v)
-    struct.pack_into("<III", ka, 160, grid, 1, 1)        # hidden_block_count_x/y/z
-    struct.pack_into("<HHH", ka, 172, threads, 1, 1)     # hidden_group_size_x/y/z
-    struct.pack_into("<H", ka, 224, 1)                   # hidden_grid_dims
+    struct.pack_into("<III", ka, ARGS_BYTES, grid, 1, 1)         # hidden_block_count_x/y/z
+    struct.pack_into("<HHH", ka, ARGS_BYTES + 12, threads, 1, 1)  # hidden_group_size_x/y/z
+    struct.pack_into("<H", ka, ARGS_BYTES + 64, 1)                # hidden_grid_dims
     return bytes(ka)
 
 
@@ -979,7 +984,7 @@ def launch(mem: Memory, asm: str, name: str, threads: int, lds_bytes: int, field
     wave-instructions executed.  Workgroups run to completion in order, so a dynamic (atomic-counter) schedule hands
     every item to the first workgroup -- functionally the same result, a different interleaving."""
     insns, labels = kernel_code(asm, name)
-    d_ka = mem.alloc(416, data=pieces_kernarg(fields, grid, threads))
+    d_ka = mem.alloc(ARGS_BYTES + 256, data=pieces_kernarg(fields, grid, threads))
     steps = 0
     for g in (range(grid) if wgs is None else wgs):
         steps += Workgroup(mem, insns, labels, threads, lds_bytes, d_ka, g).run()
@@ -989,8 +994,11 @@ def launch(mem: Memory, asm: str, name: str, threads: int, lds_bytes: int, field
 SENTINEL = 0xDEADBEEF
 
 
-def batch_memory(data, off, ln, tabs: bytes, expect=None):
-    """Device image of one batch call: payload, descriptors, results (sentinel-filled), tables, verify words."""
+def batch_memory(data, off, ln, tabs: bytes, expect=None, arrived: int = 0):
+    """Device image of one batch call: payload, descriptors, results (sentinel-filled), tables, verify words.  The
+    caller's result words start as a sentinel (the kernels must write them); the accumulators in their reset state,
+    except that `arrived` workgroups are counted as having arrived already (so one emulated workgroup of a larger grid
+    can be the last, publishing one)."""
     n = int(np.asarray(off).size)
     mem = Memory()
     f = {"base": mem.alloc(data.size + 65536, data=data), "off": mem.alloc(8 * n, data=np.asarray(off, np.uint64)),
@@ -999,28 +1007,43 @@ def batch_memory(data, off, ln, tabs: bytes, expect=None):
          "max_pieces": n, "static_contig": 1, "tabs": mem.alloc(len(tabs), data=tabs)}
     if expect is not None:
         f["expect"] = mem.alloc(4 * n, data=np.asarray(expect, np.uint32))
-        f["first_bad"] = mem.alloc(8, data=np.array([~np.uint64(0)], np.uint64))
-        f["nbad"] = mem.alloc(8)
+        f["first_bad"] = mem.alloc(8, data=np.array([SENTINEL], np.uint64))
+        f["nbad"] = mem.alloc(8, data=np.array([SENTINEL], np.uint64))
+        f["vacc"] = mem.alloc(16, data=np.array([~np.uint64(0), np.uint64(arrived) << np.uint64(40)], np.uint64))
+        f["publish"] = 1
     return mem, f
 
 
-def batch_results(mem: Memory, f: dict):
-    """(out words, mask of blocks written, first_bad or -1, nbad)"""
+def accumulators(mem: Memory, f: dict):
+    """The verify accumulators (vacc[0] = lowest posted block, vacc[1] = arrivals << 40 | mismatches)."""
+    return mem.r64(f["vacc"]), mem.r64(f["vacc"] + 8)
+
+
+def batch_results(mem: Memory, f: dict, published: bool = True):
+    """(out words, mask of blocks written, first_bad or -1, nbad); a verify call must also leave its accumulators in
+    their reset state (~0, 0) for the next call"""
     out = mem.view(f["out"], 4 * f["count"]).view(np.uint32).copy()
     fb = mem.r64(f["first_bad"]) if "first_bad" in f else (1 << 64) - 1
     nb = mem.r64(f["nbad"]) if "nbad" in f else 0
+    if published and "vacc" in f and accumulators(mem, f) != ((1 << 64) - 1, 0):
+        raise EmuError("verify accumulators not reset: %#x %#x" % accumulators(mem, f))
     # a written word equals the sentinel only by chance (1 in 2^32): callers compare against the oracle
     return out, out != SENTINEL, (-1 if fb == (1 << 64) - 1 else fb), nb
 
 
 def run_batch_kernel(asm: str, name: str, threads: int, data: np.ndarray, off, ln, tabs: bytes, wg: int = 0,
-                     grid: int = 256, hint: int = 0, expect=None, lds_bytes: int = 160768):
+                     grid: int = 256, hint: int = 0, expect=None, lds_bytes: int = 160768, last: bool = True,
+                     state: dict | None = None):
     """Run workgroup `wg` of a batch kernel (a PiecesArgs kernel in static, unplanned mode) over the given batch.
+    Verify form: with `last` the other grid - 1 workgroups count as arrived, so this one publishes the verdict; without
+    it, it is an early one and `state` (a dict) receives the accumulators it leaves.
     Returns (out words, mask of blocks written, first_bad or -1, nbad, instructions executed)."""
-    mem, f = batch_memory(data, off, ln, tabs, expect)
+    mem, f = batch_memory(data, off, ln, tabs, expect, arrived=grid - 1 if last else 0)
     f["hint"] = hint
     steps = launch(mem, asm, name, threads, lds_bytes, f, grid, [wg])
-    return batch_results(mem, f) + (steps,)
+    if state is not None and "vacc" in f:
+        state["vacc"] = accumulators(mem, f)
+    return batch_results(mem, f, published=last) + (steps,)
 
 
 # DevTables field offsets (bytes), csrc/crc32c_device.hip
@@ -1042,6 +1065,7 @@ def run_planned_batch(asm: str, pieces: str, combine: str, data: np.ndarray, off
     npieces = int(pstart[-1])
     pblk = np.repeat(np.arange(n, dtype=np.uint32), counts.astype(np.int64))
     mem, f = batch_memory(data, off, ln, tabs, expect)
+    f["publish"] = 0  # a split batch: the combine kernel publishes (its last workgroup)
     f.update(pstart=mem.alloc(8 * (n + 1), data=pstart), pblk=mem.alloc(4 * npieces, data=pblk),
              partial=mem.alloc(4 * npieces), work_counter=mem.alloc(16), piece_bytes=P, max_pieces=npieces,
              zpiece=f["tabs"] + TAB_ZSMALL + 4096 * piece_k, guided_div=0, guided_cap=0)

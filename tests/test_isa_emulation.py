@@ -79,7 +79,25 @@ def test_emulated_kernel_matches_oracle(env, label, tmpl, threads, kind):
                                                     expect=stored)
     assert np.array_equal(np.nonzero(written_v)[0], mine)
     assert np.array_equal(out_v[mine], exp[mine])
-    assert (fb, nb) == (int(plant.min()), 3)
+    assert (fb, nb) == (int(plant.min()), 3)  # published by this (last) workgroup, accumulators reset (batch_results)
+    _verify_tail(E, tmpl % 1, threads, data, off, ln, tabs, wg, hint, exp, mask, mine, plant)
+
+
+def _verify_tail(E, name, threads, data, off, ln, tabs, wg, hint, exp, mask, mine, plant, lds_bytes=160768):
+    """The verify form's end (verify_publish): a clean batch publishes (-1, 0) from the last workgroup; a workgroup that
+    is not the last leaves the caller's words alone and its posts -- lowest index, count, one arrival -- in the
+    accumulators for the last one."""
+    clean = np.array([mask(int(x)) for x in exp], np.uint32)
+    *_, fb, nb, _ = E.run_batch_kernel(ASM, name, threads, data, off, ln, tabs, wg=wg, hint=hint, expect=clean,
+                                       lds_bytes=lds_bytes)
+    assert (fb, nb) == (-1, 0)
+    stored = clean.copy()
+    stored[plant] ^= 0x100
+    st = {}
+    *_, fb, nb, _ = E.run_batch_kernel(ASM, name, threads, data, off, ln, tabs, wg=wg, hint=hint, expect=stored,
+                                       lds_bytes=lds_bytes, last=False, state=st)
+    assert (fb, nb) == (E.SENTINEL, E.SENTINEL)  # not published
+    assert st["vacc"] == (int(plant.min()), (1 << 40) | len(plant)), [hex(v) for v in st["vacc"]]
 
 
 PIECES = "_ZN5kvsep20crc32c_pieces_kernelILb%dELb%dELi4ELb1ELb1ELi0ELi512ELb1ELb%dEEEvNS_10PiecesArgsE"
@@ -114,6 +132,7 @@ def test_emulated_wide_unplanned(env, verify):
                                                   expect=_planted(exp, mask, plant))
         assert np.array_equal(np.nonzero(wv)[0], mine) and np.array_equal(out_v[mine], exp[mine])
         assert (fb, nb) == (int(plant.min()), 2)
+        _verify_tail(E, PIECES % (0, 0, 1), 512, data, off, ln, tabs, 7, 0, exp, mask, mine, plant)
 
 
 @pytest.mark.parametrize("verify", [0, 1])
@@ -138,4 +157,7 @@ def test_emulated_wide_planned_with_combine(env, verify):
     assert written.all()
     assert np.array_equal(out, exp), f"{np.count_nonzero(out != exp)} wrong CRCs"
     if verify:
-        assert (fb, nb) == (2, 3)
+        assert (fb, nb) == (2, 3)  # the combine kernel's last workgroup published; accumulators reset (batch_results)
+        _, _, fb, nb, _ = E.run_planned_batch(ASM, PIECES % (1, 1, 1), COMBINE % 1, data, off, ln, tabs,
+                                              expect=_planted(exp, mask, np.array([], np.int64)))
+        assert (fb, nb) == (-1, 0)
