@@ -89,11 +89,10 @@ struct PiecesArgs {
   unsigned long long* first_bad;
   unsigned long long* nbad;
   const DevTables* tabs;
-  // The context's accumulator words, kept in their reset state between calls: vacc[0] = lowest mismatching block
-  // (~0: none), vacc[1] = (workgroups arrived << 40) | mismatches.  Mismatches post there (atomicMin / atomicAdd); the
-  // last workgroup to arrive copies them to first_bad / nbad and resets them, so a verify call needs no init launch.
+  // The context's accumulator words, kept in their reset state between calls (layout at vacc_shard): mismatches post
+  // there (atomicMin / atomicAdd); the last workgroup to arrive copies the verdict to first_bad / nbad and resets them,
+  // so a verify call needs no init launch.
   unsigned long long* vacc;
-  uint32_t publish;  // the pieces kernel publishes (an unsplit batch) or leaves it to the combine kernel (a split one)
 };
 
 // Descriptor reads through the constant address space: wave-uniform indices then lower to scalar
@@ -419,14 +418,28 @@ __device__ uint32_t gf2_shift(const DevTables* tabs, uint32_t reg, uint64_t n) {
 
 __device__ __forceinline__ void emit_block(const PiecesArgs& a, uint64_t b, uint32_t crc) { a.out[b] = crc; }
 
+// The verify form's accumulators (PiecesArgs::vacc, u64 words, each group on a 128-B line of its own): [0] the lowest
+// mismatching block (~0: none); [1] the final arrival word, (arrivals << 40) | mismatches: every mismatch count is
+// posted there, so the count travels with the arrivals; and at [16 (s + 1)] the arrival word of shard s = blockIdx.x
+// mod 8 (one shard per XCD: the dispatcher deals workgroups round-robin over the 8 XCDs), used by grids whose
+// workgroups arrive together (verify_publish).
+constexpr uint32_t kVaccShards = 8, kVaccStride = 16;  // 16 words = 128 B
+constexpr unsigned long long kArrive = 1ull << 40, kCountMask = kArrive - 1;
+
+// A wave that posted a mismatch waits, right there, until its posts are performed (the rare path: it drains the wave's
+// staged loads once), so the end of the kernel needs no wait before the workgroup arrives (verify_publish): a clean
+// workgroup arrives while its last result stores are still in flight.  Atomic against atomic, a completed post is all
+// the order needs.  Not __threadfence(): on gfx950 that is an L2 writeback + invalidate (buffer_wbl2 / buffer_inv sc1),
+// which at the end of every wave cost 130-170 us per launch (measured).
+__device__ __forceinline__ void post_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // The verify form fused into the CRC kernels (db/value_log_reader.cc:109-122, table/format.cc:99-106).  Called by the
 // whole wave (full EXEC) right after a group's emit: lanes with `mine` hold block b's crc and the stored word `ex`
 // they loaded before the next group's staging (so waiting for it never drains those loads).  The compare itself is
 // branch-free; the wave ballots the mismatches and only a mismatch enters a wave-uniform branch, where one lane posts
-// the wave's lowest mismatching index and the count to the accumulator words (fenced at the end of the kernel, before
-// the workgroup arrives: verify_publish).  A per-lane branch on the compare nested
-// inside the emit's divergent branch is what made the round-1 sorted-window kernel miscompute.
-// The lane's block is base + idx (base wave-uniform): one VGPR for the index, not a 64-bit pair.
+// the wave's lowest mismatching index (vacc[0]) and the count (vacc[1]).  A per-lane branch on the
+// compare nested inside the emit's divergent branch is what made the round-1 sorted-window kernel miscompute (DESIGN
+// §3.5).  The lane's block is base + idx (base wave-uniform): one VGPR for the index, not a 64-bit pair.
 __device__ __forceinline__ void verify_wave(const PiecesArgs& a, uint32_t lane, bool mine, uint64_t base, uint32_t idx,
                                             uint32_t crc, uint32_t ex) {
   const uint64_t m = __builtin_amdgcn_ballot_w64(mine && mask_crc(crc) != ex);
@@ -440,45 +453,61 @@ __device__ __forceinline__ void verify_wave(const PiecesArgs& a, uint32_t lane, 
       atomicMin(a.vacc, (unsigned long long)(base + best));
       atomicAdd(a.vacc + 1, (unsigned long long)__builtin_popcountll(m));
     }
+    post_wait();
   }
 }
 
 // One block checked by a whole wave whose crc and stored word are wave-uniform (the wide kernel, the deferred walk).
 __device__ __forceinline__ void verify_uniform(const PiecesArgs& a, uint32_t lane, uint64_t b, uint32_t crc,
                                                uint32_t ex) {
-  if (__builtin_amdgcn_ballot_w64(mask_crc(crc) != ex)) {  // wave-uniform
-    if (lane == 0) {
-      atomicMin(a.vacc, (unsigned long long)b);
-      atomicAdd(a.vacc + 1, 1ull);
-    }
+  if (mask_crc(crc) != ex && lane == 0) {
+    atomicMin(a.vacc, (unsigned long long)b);
+    atomicAdd(a.vacc + 1, 1ull);
+    post_wait();
   }
 }
 
-// The end of a publishing verify kernel, every workgroup: once its waves are done and have fenced their posts, wave 0
-// arrives on vacc[1] with one returning atomic; the last workgroup to arrive copies the verdict to
-// the caller's first_bad / nbad and puts the accumulators back in their reset state (~0, 0) for the next call.  The
-// mismatch count travels in the arrival word, so a clean batch costs the last workgroup one atomic round trip;
-// vacc[0] is read (and reset) only when something mismatched.  This replaces a separate init launch per call.
+// One returning device-scope atomic add by lane 0, its old value broadcast (wave-uniform).
+__device__ __forceinline__ unsigned long long arrive(unsigned long long* w, unsigned long long v, uint32_t lane) {
+  unsigned long long old = 0;
+  if (lane == 0) old = atomicAdd(w, v);
+  return (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(old >> 32)), 0))) << 32) |
+         uint32_t(__builtin_amdgcn_readlane(int(uint32_t(old)), 0));
+}
+
+// The end of a publishing verify kernel (the CRC kernel of an unsplit batch, the combine kernel of a split one), every
+// workgroup: once its waves are done with their posts, wave 0 arrives on the final word; the last workgroup to arrive
+// copies the verdict to the caller's first_bad / nbad and puts the accumulators back in their reset state (~0, 0) for
+// the next call.  So a verify call needs no init launch, and a clean batch costs its last workgroup one atomic round
+// trip (vacc[0] is read, and reset, only when something mismatched).
+// kShards = 8: the workgroups arrive first on their shard's word and only each shard's last on the final word.  For a
+// grid whose workgroups all arrive at once (the combine kernel): 256 arrivals on ONE word queue at ~11-13 ns each
+// (MI355X_MICROARCH.md fanin: 3.2-4.5 us; measured +2.7 us on the combine kernel).  The CRC kernels' workgroups end
+// over several us (issue-age staircase), so they take one level: one round trip less for the last one.
 // `wave`: the wave's index in the workgroup (wave-uniform, an SGPR); the lane is recomputed here (v_mbcnt) rather than
 // kept live from the kernel's start: at the 16-wave kernels' 128-VGPR cap one more long-lived VGPR spills.
+template <uint32_t kShards = 1>
 __device__ __forceinline__ void verify_publish(const PiecesArgs& a, uint32_t wave) {
-  __threadfence();  // this wave's posts (if any) are performed before the workgroup arrives
-  __syncthreads();
-  if (wave == 0) {
-    uint32_t lane;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-    unsigned long long old = 0;
-    if (lane == 0) old = atomicAdd(a.vacc + 1, 1ull << 40);
-    old = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(old >> 32)), 0))) << 32) |
-          uint32_t(__builtin_amdgcn_readlane(int(uint32_t(old)), 0));
-    if ((old >> 40) + 1 == gridDim.x && lane == 0) {  // the last workgroup
-      const unsigned long long nb = old & ((1ull << 40) - 1);
-      atomicExch(a.vacc + 1, 0ull);  // first, so the wait for the swap's result below is a plain vmcnt(0)
-      const unsigned long long fb = nb ? atomicExch(a.vacc, ~0ull) : ~0ull;
-      *a.first_bad = fb;
-      *a.nbad = nb;
-    }
+  __syncthreads();  // every wave of the workgroup is done; any that posted has waited for its posts (post_wait)
+  if (wave != 0) return;
+  uint32_t lane;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+  uint32_t arrivals = gridDim.x;  // expected on the final word
+  if (kShards > 1) {
+    const uint32_t shard = blockIdx.x % kShards;
+    unsigned long long* sw = a.vacc + kVaccStride * (1 + shard);
+    const unsigned long long o1 = arrive(sw, kArrive, lane);
+    if ((o1 >> 40) + 1 != (gridDim.x - shard + kShards - 1) / kShards) return;  // not the shard's last
+    if (lane == 0) atomicExch(sw, 0ull);  // the shard word back to its reset state
+    arrivals = gridDim.x < kShards ? gridDim.x : kShards;
   }
+  const unsigned long long old = arrive(a.vacc + 1, kArrive, lane);
+  if ((old >> 40) + 1 != arrivals || lane != 0) return;  // the last workgroup of all, lane 0
+  const unsigned long long nb = old & kCountMask;
+  atomicExch(a.vacc + 1, 0ull);  // first, so the wait for the swap's result below is a plain vmcnt(0)
+  const unsigned long long fb = nb ? atomicExch(a.vacc, ~0ull) : ~0ull;
+  *a.first_bad = fb;
+  *a.nbad = nb;
 }
 
 // A 32-bit global load (address space 1), for the stored words of the verify form.
@@ -755,7 +784,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
       else a.partial[it.g] = reg;
     }
     // lane 0 holds the register: its readlane makes the compare, and the branch on it, wave-uniform
-    if (kVerify && it.only) verify_uniform(a, lane, it.b, ~uint32_t(__builtin_amdgcn_readlane(int(reg), 0)), it.exp);
+    if (kVerify && it.only)
+      verify_uniform(a, lane, it.b, ~uint32_t(__builtin_amdgcn_readlane(int(reg), 0)), it.exp);
   };
 
   // One item: finish item g (staged in A) while item g+1 is staged into B.  The loop below alternates the
@@ -792,7 +822,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
     }
   }
   KVSEP_WSTAMP_EXIT();
-  if (kVerify && a.publish) verify_publish(a, wave);
+  if (kVerify && !kPlanned) verify_publish(a, wave);  // a split batch's verdict is the combine kernel's to publish
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1407,7 +1437,7 @@ __global__ void __launch_bounds__(256) crc32c_combine_kernel(PiecesArgs a) {
   }
   if (kVerify) {
     verify_wave(a, threadIdx.x & 63u, mine, uint64_t(blockIdx.x) * 256, threadIdx.x, crc, ld32(a.expect + bb));
-    verify_publish(a, threadIdx.x >> 6);  // the split blocks' verdict: after the CRC kernel's whole-block posts
+    verify_publish<kVaccShards>(a, threadIdx.x >> 6);  // after the CRC kernel's whole-block posts
   }
 }
 
@@ -1625,14 +1655,17 @@ int release(Scratch& sc, hipStream_t s) {
   return KVSEP_OK;
 }
 
-// The verify form's device words (32 B, allocated once per scratch, before any capture -- kvsep_crc32c_reserve does it):
-// [0] / [1] the result words of a call whose caller passes none, [2] / [3] the accumulators the kernels post to and
-// reset (PiecesArgs::vacc), which must start in their reset state: ~0 (no mismatch) and 0 (nothing arrived, none bad).
+// The verify form's device words (allocated once per scratch, before any capture -- kvsep_crc32c_reserve does it): on
+// the first 128-B line the result words of a call whose caller passes none; then the accumulators the kernels post to
+// and reset (PiecesArgs::vacc: the lowest-block word and the final arrival word, then 8 shard arrival words, each group
+// on a line of its own), which must start in their reset state: ~0 (no mismatch), 0 (nothing arrived, none bad).
 int ensure_verify(Scratch& sc) {
   if (sc.d_verify) return KVSEP_OK;
-  const unsigned long long init[4] = {~0ull, 0ull, ~0ull, 0ull};
-  KVSEP_HIP(hipMalloc(&sc.d_verify, sizeof init));
-  KVSEP_HIP(hipMemcpy(sc.d_verify, init, sizeof init, hipMemcpyHostToDevice));
+  std::vector<unsigned long long> init(kVaccStride * (2 + kVaccShards), 0ull);
+  init[0] = ~0ull;            // default first_bad
+  init[kVaccStride] = ~0ull;  // vacc[0]
+  KVSEP_HIP(hipMalloc(&sc.d_verify, init.size() * 8));
+  KVSEP_HIP(hipMemcpy(sc.d_verify, init.data(), init.size() * 8, hipMemcpyHostToDevice));
   return KVSEP_OK;
 }
 
@@ -1826,7 +1859,7 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
       first_bad = reinterpret_cast<uint64_t*>(sc.d_verify);
       nbad = reinterpret_cast<uint64_t*>(sc.d_verify + 1);
     }
-    a.vacc = sc.d_verify + 2;  // the accumulators, in their reset state: the kernels publish the verdict (no init)
+    a.vacc = sc.d_verify + kVaccStride;  // the accumulators, in their reset state: the kernels publish the verdict
     if (count == 0) {          // nothing to check, no kernel: the verdict is "none" (first_bad = ~0, nbad = 0)
       KVSEP_HIP(hipMemsetAsync(first_bad, 0xff, 8, s));
       KVSEP_HIP(hipMemsetAsync(nbad, 0, 8, s));
@@ -1835,7 +1868,6 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
   a.expect = expect;
   a.first_bad = reinterpret_cast<unsigned long long*>(first_bad);
   a.nbad = reinterpret_cast<unsigned long long*>(nbad);
-  a.publish = planned ? 0u : 1u;  // a split batch's verdict is published by the combine kernel
   // The verify form's compare runs inside the CRC kernels (and the combine kernel for split blocks): `fused`.  Only
   // the A/B variants of the KVSEP_DIAG tools build fall back to the separate verify_finish_kernel pass.
   bool fused = true;

@@ -856,6 +856,10 @@ class Workgroup:
             a, sh, b = V(o[1]), V(o[2]) & u(31), V(o[3])
             w.vset(o[0], (a << sh) | b)
             return
+        if base == 'v_mad_u32_u24':
+            a, b, c = V(o[1]) & u(0xFFFFFF), V(o[2]) & u(0xFFFFFF), V(o[3])
+            w.vset(o[0], ((a.astype(np.uint64) * b.astype(np.uint64) + c) & np.uint64(M32)).astype(np.uint32))
+            return
         if base == 'v_lshl_add_u32':
             a, sh, b = V(o[1]), V(o[2]) & u(31), V(o[3])
             w.vset(o[0], ((a << sh) + b) & u(M32))
@@ -953,8 +957,11 @@ class Workgroup:
 PIECES_ARGS = {"base": 0, "off": 8, "len": 16, "init": 24, "out": 32, "count": 40, "pstart": 48, "pblk": 56,
                "partial": 64, "work_counter": 72, "piece_bytes": 80, "zpiece": 88, "max_pieces": 96,
                "static_contig": (104, "<I"), "guided_div": (108, "<I"), "guided_cap": (112, "<I"), "hint": 120,
-               "expect": 128, "first_bad": 136, "nbad": 144, "tabs": 152, "vacc": 160, "publish": (168, "<I")}
-ARGS_BYTES = 176
+               "expect": 128, "first_bad": 136, "nbad": 144, "tabs": 152, "vacc": 160}
+ARGS_BYTES = 168
+# the verify accumulators (crc32c_device.hip, PiecesArgs::vacc): u64 words; [0] lowest block, [1] final arrival word
+# (arrived << 40) | mismatches, shard s's arrival word at [16 (s + 1)] (the combine kernel's two-level arrival)
+VACC_STRIDE, VACC_SHARDS = 16, 8
 
 
 def pieces_kernarg(fields: dict, grid: int, threads: int) -> bytes:
@@ -994,11 +1001,11 @@ def launch(mem: Memory, asm: str, name: str, threads: int, lds_bytes: int, field
 SENTINEL = 0xDEADBEEF
 
 
-def batch_memory(data, off, ln, tabs: bytes, expect=None, arrived: int = 0):
+def batch_memory(data, off, ln, tabs: bytes, expect=None, last_of=None):
     """Device image of one batch call: payload, descriptors, results (sentinel-filled), tables, verify words.  The
     caller's result words start as a sentinel (the kernels must write them); the accumulators in their reset state,
-    except that `arrived` workgroups are counted as having arrived already (so one emulated workgroup of a larger grid
-    can be the last, publishing one)."""
+    except with last_of = (wg, grid): every other workgroup of the grid counts as arrived already (its shard's and the
+    other shards'), so emulating that one workgroup is the last, publishing one."""
     n = int(np.asarray(off).size)
     mem = Memory()
     f = {"base": mem.alloc(data.size + 65536, data=data), "off": mem.alloc(8 * n, data=np.asarray(off, np.uint64)),
@@ -1009,14 +1016,19 @@ def batch_memory(data, off, ln, tabs: bytes, expect=None, arrived: int = 0):
         f["expect"] = mem.alloc(4 * n, data=np.asarray(expect, np.uint32))
         f["first_bad"] = mem.alloc(8, data=np.array([SENTINEL], np.uint64))
         f["nbad"] = mem.alloc(8, data=np.array([SENTINEL], np.uint64))
-        f["vacc"] = mem.alloc(16, data=np.array([~np.uint64(0), np.uint64(arrived) << np.uint64(40)], np.uint64))
-        f["publish"] = 1
+        v = np.zeros(VACC_STRIDE * (1 + VACC_SHARDS), np.uint64)
+        v[0] = ~np.uint64(0)
+        if last_of is not None:  # the CRC kernels arrive on the final word directly (one level)
+            wg, grid = last_of
+            v[1] = np.uint64(grid - 1) << np.uint64(40)
+        f["vacc"] = mem.alloc(8 * v.size, data=v)
     return mem, f
 
 
 def accumulators(mem: Memory, f: dict):
-    """The verify accumulators (vacc[0] = lowest posted block, vacc[1] = arrivals << 40 | mismatches)."""
-    return mem.r64(f["vacc"]), mem.r64(f["vacc"] + 8)
+    """The verify accumulators: (lowest posted block, final arrival word, the 8 shard arrival words)."""
+    return (mem.r64(f["vacc"]), mem.r64(f["vacc"] + 8)) + tuple(
+        mem.r64(f["vacc"] + 8 * VACC_STRIDE * (1 + s)) for s in range(VACC_SHARDS))
 
 
 def batch_results(mem: Memory, f: dict, published: bool = True):
@@ -1025,8 +1037,8 @@ def batch_results(mem: Memory, f: dict, published: bool = True):
     out = mem.view(f["out"], 4 * f["count"]).view(np.uint32).copy()
     fb = mem.r64(f["first_bad"]) if "first_bad" in f else (1 << 64) - 1
     nb = mem.r64(f["nbad"]) if "nbad" in f else 0
-    if published and "vacc" in f and accumulators(mem, f) != ((1 << 64) - 1, 0):
-        raise EmuError("verify accumulators not reset: %#x %#x" % accumulators(mem, f))
+    if published and "vacc" in f and accumulators(mem, f) != ((1 << 64) - 1,) + (0,) * (1 + VACC_SHARDS):
+        raise EmuError("verify accumulators not reset: %s" % [hex(x) for x in accumulators(mem, f)])
     # a written word equals the sentinel only by chance (1 in 2^32): callers compare against the oracle
     return out, out != SENTINEL, (-1 if fb == (1 << 64) - 1 else fb), nb
 
@@ -1038,7 +1050,7 @@ def run_batch_kernel(asm: str, name: str, threads: int, data: np.ndarray, off, l
     Verify form: with `last` the other grid - 1 workgroups count as arrived, so this one publishes the verdict; without
     it, it is an early one and `state` (a dict) receives the accumulators it leaves.
     Returns (out words, mask of blocks written, first_bad or -1, nbad, instructions executed)."""
-    mem, f = batch_memory(data, off, ln, tabs, expect, arrived=grid - 1 if last else 0)
+    mem, f = batch_memory(data, off, ln, tabs, expect, last_of=(wg, grid) if last else None)
     f["hint"] = hint
     steps = launch(mem, asm, name, threads, lds_bytes, f, grid, [wg])
     if state is not None and "vacc" in f:
@@ -1064,12 +1076,13 @@ def run_planned_batch(asm: str, pieces: str, combine: str, data: np.ndarray, off
     pstart[1:] = np.cumsum(counts, dtype=np.uint64)
     npieces = int(pstart[-1])
     pblk = np.repeat(np.arange(n, dtype=np.uint32), counts.astype(np.int64))
-    mem, f = batch_memory(data, off, ln, tabs, expect)
-    f["publish"] = 0  # a split batch: the combine kernel publishes (its last workgroup)
+    mem, f = batch_memory(data, off, ln, tabs, expect)  # a split batch: the combine kernel's last workgroup publishes
     f.update(pstart=mem.alloc(8 * (n + 1), data=pstart), pblk=mem.alloc(4 * npieces, data=pblk),
              partial=mem.alloc(4 * npieces), work_counter=mem.alloc(16), piece_bytes=P, max_pieces=npieces,
              zpiece=f["tabs"] + TAB_ZSMALL + 4096 * piece_k, guided_div=0, guided_cap=0)
-    steps = launch(mem, asm, pieces, 512, 160768, f, grid, [0])
+    # one workgroup takes every item; not workgroup 0, so its shard (5) is one the combine grid below may not have:
+    # the planned kernel's counts must reach the publishing grid anyway
+    steps = launch(mem, asm, pieces, 512, 160768, f, grid, [5])
     steps += launch(mem, asm, combine, 256, 4096, f, (n + 255) // 256)
     return batch_results(mem, f) + (steps,)
 

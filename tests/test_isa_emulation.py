@@ -97,7 +97,8 @@ def _verify_tail(E, name, threads, data, off, ln, tabs, wg, hint, exp, mask, min
     *_, fb, nb, _ = E.run_batch_kernel(ASM, name, threads, data, off, ln, tabs, wg=wg, hint=hint, expect=stored,
                                        lds_bytes=lds_bytes, last=False, state=st)
     assert (fb, nb) == (E.SENTINEL, E.SENTINEL)  # not published
-    assert st["vacc"] == (int(plant.min()), (1 << 40) | len(plant)), [hex(v) for v in st["vacc"]]
+    # one arrival and the count on the final word; the shard words belong to the combine kernel's two-level arrival
+    assert st["vacc"] == (int(plant.min()), (1 << 40) | len(plant)) + (0,) * E.VACC_SHARDS, [hex(v) for v in st["vacc"]]
 
 
 PIECES = "_ZN5kvsep20crc32c_pieces_kernelILb%dELb%dELi4ELb1ELb1ELi0ELi512ELb1ELb%dEEEvNS_10PiecesArgsE"
