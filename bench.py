@@ -149,6 +149,11 @@ class RefBatch:
         self.lib.ref_crc32c_batch.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_int]
         self.lib.ref_crc32c_batch.restype = ctypes.c_int
 
+        f = self.lib.ref_crc32c_timed_local
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_double,
+                                              ctypes.c_void_p, ctypes.c_void_p]
+
     def batch(self, buf, off, length, init=None, threads=1):
         out = np.zeros(off.size, dtype=np.uint32)
         off = np.ascontiguousarray(off, dtype=np.uint64)
@@ -156,6 +161,17 @@ class RefBatch:
         assert self.lib.ref_crc32c_batch(buf.ctypes.data, off.ctypes.data, length.ctypes.data, None,
                                          out.ctypes.data, off.size, threads) == 0
         return out
+
+    def timed_local(self, buf, off, length, cpus, seconds):
+        """ref_crc32c_timed_local: len(cpus) threads, thread t pinned to cpus[t], each on its own first-touched copy of
+        its byte-balanced block range, repeated passes for `seconds` -> (bytes, elapsed s)."""
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint64)
+        c = np.ascontiguousarray(cpus, dtype=np.int32)
+        b, t = ctypes.c_uint64(), ctypes.c_double()
+        assert self.lib.ref_crc32c_timed_local(buf.ctypes.data, off.ctypes.data, length.ctypes.data, off.size, c.size,
+                                               c.ctypes.data, seconds, ctypes.byref(b), ctypes.byref(t)) == 0
+        return b.value, t.value
 
 
 def cpu_model() -> str:
@@ -169,9 +185,74 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _cpulist(text):
+    out = []
+    for part in (text or "").split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            out.extend(range(int(a), int(b) + 1))
+        elif part.strip():
+            out.append(int(part))
+    return out
+
+
+def cpu_quota():
+    """The cgroup CPU limit this process runs under: cgroup v2 cpu.max ("quota period" or "max period"), else v1
+    cfs_quota_us / cfs_period_us -> (raw text, CPUs or None when unlimited)."""
+    v2 = _read("/sys/fs/cgroup/cpu.max")
+    if v2:
+        q, per = (v2.split() + ["100000"])[:2]
+        return v2, (None if q == "max" else int(q) / int(per))
+    q, per = _read("/sys/fs/cgroup/cpu/cpu.cfs_quota_us"), _read("/sys/fs/cgroup/cpu/cpu.cfs_period_us")
+    if q and per:
+        return f"cfs_quota_us={q} cfs_period_us={per}", (None if int(q) < 0 else int(q) / int(per))
+    return None, None
+
+
+def numa_nodes():
+    """{node: [cpus]} from /sys/devices/system/node (one node "0" with every CPU when absent)."""
+    base = "/sys/devices/system/node"
+    nodes = {}
+    try:
+        for d in sorted(os.listdir(base)):
+            if d.startswith("node") and d[4:].isdigit():
+                nodes[int(d[4:])] = _cpulist(_read(os.path.join(base, d, "cpulist")))
+    except OSError:
+        pass
+    return nodes or {0: list(range(os.cpu_count() or 1))}
+
+
+def spread_cpus(allowed):
+    """The CPUs this process may run on, ordered so that any prefix spreads over the NUMA nodes (round-robin) and
+    takes one hardware thread of each physical core before any SMT sibling."""
+    node_of = {c: n for n, cs in numa_nodes().items() for c in cs}
+    per_node = {}
+    for c in sorted(allowed):
+        sib = _cpulist(_read(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list")) or [c]
+        rank = sorted(sib).index(c) if c in sib else 0  # 0: the core's first hardware thread
+        per_node.setdefault(node_of.get(c, 0), []).append((rank, c))
+    queues = [sorted(v) for _, v in sorted(per_node.items())]
+    order = []
+    while any(queues):
+        for q in queues:
+            if q:
+                order.append(q.pop(0)[1])
+    return order, node_of
+
+
 def cpu_baseline(oracle, data_dev, off, ln, sample_blocks, thread_counts, seconds):
     """CPU CRC on host cores over a sample of the batch: the compiled reference (kind "reference") when oracle/_ref
-    was built, else the oracle restatement (kind "port"), at each thread count in `thread_counts`."""
+    was built, else the oracle restatement (kind "port"), at each thread count in `thread_counts`.  The reference runs
+    through ref_crc32c_timed_local: threads pinned spread over the NUMA nodes (spread_cpus), each checksumming its own
+    first-touched copy of its byte range, so every thread reads memory local to it."""
     idx = np.linspace(0, off.size - 1, sample_blocks).astype(np.int64)
     lens = ln[idx]
     host = np.empty(int(lens.sum()), dtype=np.uint8)
@@ -186,6 +267,13 @@ def cpu_baseline(oracle, data_dev, off, ln, sample_blocks, thread_counts, second
     impl, kind = oracle, "port"
     if os.path.exists(RefBatch.PATH):
         impl, kind = RefBatch(), "reference"
+        order, node_of = spread_cpus(os.sched_getaffinity(0))
+        impl.batch(host, hoff[:8], lens[:8], threads=1)  # warm tables
+        for t in thread_counts:
+            cpus = order[:t] if t <= len(order) else (order * (t // len(order) + 1))[:t]
+            nb, dt = impl.timed_local(host, hoff, lens, cpus, seconds)
+            out[t] = (nb / GIB / dt, nb, dt, sorted({node_of.get(c, 0) for c in cpus}))
+        return out, host, hoff, lens, idx, kind
     for t in thread_counts:
         sub = sample_blocks if t > 1 else max(1, sample_blocks // 4)
         sb = int(lens[:sub].sum())
@@ -198,7 +286,7 @@ def cpu_baseline(oracle, data_dev, off, ln, sample_blocks, thread_counts, second
             dt = time.perf_counter() - t0
             if dt >= seconds:
                 break
-        out[t] = (passes * sb / GIB / dt, passes * sb, dt)
+        out[t] = (passes * sb / GIB / dt, passes * sb, dt, None)
     return out, host, hoff, lens, idx, kind
 
 
@@ -611,22 +699,35 @@ def main():
         if not args.no_cpu and world == 1:
             aff = len(os.sched_getaffinity(0))
             most = args.cpu_threads or aff
-            counts = sorted({1, most} | {t for t in (16, 32, 64, 128) if t < most})
+            quota_raw, quota = cpu_quota()
+            counts = {1, most} | {t for t in (8, 16, 32, 64, 128) if t < most}
+            if quota and int(quota) < most:
+                counts.add(max(1, int(quota)))  # the cgroup's CPU share: the scaling must flatten there
+            counts = sorted(counts)
             nsample = min(args.cpu_sample_blocks, count)
             res, host, hoff, lens, idx, kind = cpu_baseline(oracle, data, off, ln, nsample, counts, args.cpu_seconds)
             threads = max(counts, key=lambda t: res[t][0])  # the baseline is the CPU's best thread count
-            vt, sbt, dtt = res[threads]
-            impl_desc = ("util/crc32c.cc of the reference (portable path, g++ -O3, oracle/_ref)"
+            vt, sbt, dtt, _ = res[threads]
+            impl_desc = ("util/crc32c.cc of the reference (portable path, g++ -O3, oracle/_ref), each thread pinned "
+                         "(spread over the NUMA nodes, one hardware thread per core first) and checksumming its own "
+                         "first-touched copy of its byte range"
                          if kind == "reference" else
                          "oracle/crc32c_oracle.c (restated util/crc32c.cc portable path, gcc -O3)")
+            nodes = numa_nodes()
             cpu = {"value": round(vt, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
                    "sample": f"{nsample} blocks of the same batch ({int(lens.sum()) / GIB:.2f} GiB) copied to host "
                              f"memory, {impl_desc}; blocks split over threads by bytes, repeated passes of "
-                             f"{args.cpu_seconds:.0f} s per thread count, 1 to {most} threads (every core this process "
+                             f"{args.cpu_seconds:.0f} s per thread count, 1 to {most} threads (every CPU this process "
                              f"may run on); best: {threads} threads, {sbt / GIB:.1f} GiB in {dtt:.1f} s",
                    "by_threads_GiBps": {str(t): round(res[t][0], 3) for t in counts},
+                   "by_threads_numa_nodes": {str(t): res[t][3] for t in counts},
                    "single_thread_GiBps": round(res[1][0], 3),
-                   "nproc": os.cpu_count(), "affinity_cores": aff, "cpu_model": cpu_model()}
+                   "nproc": os.cpu_count(), "affinity_cores": aff, "cpu_model": cpu_model(),
+                   "cgroup_cpu_max": quota_raw, "cgroup_cpu_limit": quota,
+                   "numa_nodes": {str(n): f"{len(c)} cpus ({c[0]}-{c[-1]})" for n, c in nodes.items() if c},
+                   "limit_note": (f"this process may use {quota:g} CPUs' worth of time (cgroup cpu.max) of the {aff} "
+                                  f"it may run on: rates flatten from {int(quota)} threads on" if quota and quota < aff
+                                  else "no cgroup CPU limit below the affinity set")}
             s1 = sse42_rate(host, hoff[:max(1, nsample // 4)], lens[:max(1, nsample // 4)], 1, 2.0)
             sn = sse42_rate(host, hoff, lens, threads, 2.0)
             cpu["sse42_crc32_GiBps"] = {"1": round(s1, 3), str(threads): round(sn, 3),

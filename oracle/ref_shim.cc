@@ -124,3 +124,126 @@ extern "C" int ref_crc32c_stream_batch(uint64_t seed, uint64_t stream_base, cons
   for (int t = 0; t < launched; ++t) pthread_join(th[t], nullptr);
   return 0;
 }
+
+// The CPU baseline of bench.py (cpu_baseline, kind "reference"): the reference Extend over a sample of blocks on
+// `nthreads` host threads for about `seconds`, each thread pinned to cpus[t] (when given) and working on its OWN copy
+// of its byte-balanced block range, made by itself before the clock starts -- first touch places those pages on the
+// thread's NUMA node, so a 2-socket box is measured on local memory instead of on the one node the shared sample sits
+// on.  Every thread passes over its range repeatedly until the common deadline; *bytes_out is the total checksummed,
+// *secs_out the elapsed time from the common start to the last thread's end.  Returns 0, or -1 if a thread or a
+// buffer could not be created.
+#include <sched.h>
+
+#include <atomic>
+#include <chrono>
+
+namespace {
+struct LocalJob {
+  const char* src; const uint64_t* off; const uint64_t* len;
+  size_t lo, hi;
+  int cpu;
+  double seconds;
+  std::atomic<int>* ready;   // threads done with their copy
+  std::atomic<int>* abort;   // set when a thread could not be created: nobody waits for it
+  int nthreads;
+  std::atomic<double>* t0;
+  uint64_t bytes = 0;
+  double end = 0;
+  uint32_t sink = 0;
+  int err = 0;
+};
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+void* local_worker(void* p) {
+  LocalJob* j = static_cast<LocalJob*>(p);
+  if (j->cpu >= 0) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(j->cpu, &set);
+    sched_setaffinity(0, sizeof set, &set);  // this thread; its later allocations follow it (first touch)
+  }
+  uint64_t total = 0;
+  for (size_t i = j->lo; i < j->hi; ++i) total += j->len[i];
+  char* mine = static_cast<char*>(std::malloc(total ? total : 1));
+  std::vector<uint64_t> loff(j->hi - j->lo);
+  if (!mine) j->err = 1;
+  else {
+    uint64_t pos = 0;
+    for (size_t i = j->lo; i < j->hi; ++i) {  // the copy is this thread's first touch of its pages
+      std::memcpy(mine + pos, j->src + j->off[i], j->len[i]);
+      loff[i - j->lo] = pos;
+      pos += j->len[i];
+    }
+  }
+  j->ready->fetch_add(1);
+  while (j->ready->load() < j->nthreads && !j->abort->load()) sched_yield();
+  double expect = 0;
+  if (j->t0->load() == 0) j->t0->compare_exchange_strong(expect, now_s());
+  const double stop = j->t0->load() + j->seconds;
+  uint32_t s = 0;
+  if (mine) {
+    do {
+      for (size_t i = j->lo; i < j->hi; ++i) s ^= leveldb::crc32c::Extend(0, mine + loff[i - j->lo], j->len[i]);
+      j->bytes += total;
+    } while (now_s() < stop);
+  }
+  j->end = now_s();
+  j->sink = s;
+  std::free(mine);
+  return nullptr;
+}
+}  // namespace
+
+extern "C" int ref_crc32c_timed_local(const char* src, const uint64_t* off, const uint64_t* len, size_t count,
+                                      int nthreads, const int* cpus, double seconds, uint64_t* bytes_out,
+                                      double* secs_out) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 1024) nthreads = 1024;
+  uint64_t total = 0;
+  for (size_t i = 0; i < count; ++i) total += len[i];
+  std::vector<LocalJob> jobs(nthreads);
+  std::vector<pthread_t> th(nthreads);
+  std::atomic<int> ready{0}, abort{0};
+  std::atomic<double> t0{0};
+  size_t start = 0;
+  uint64_t acc = 0;
+  int n = 0;
+  for (int t = 0; t < nthreads && start < count; ++t, ++n) {
+    const uint64_t target = (total / uint64_t(nthreads)) * uint64_t(t + 1);
+    size_t stop = start;
+    if (t == nthreads - 1) stop = count;
+    else
+      while (stop < count && acc < target) acc += len[stop++];
+    if (stop == start && stop < count) acc += len[stop++];  // at least one block per thread
+    jobs[t].src = src; jobs[t].off = off; jobs[t].len = len;
+    jobs[t].lo = start; jobs[t].hi = stop;
+    jobs[t].cpu = cpus ? cpus[t] : -1;
+    jobs[t].seconds = seconds;
+    jobs[t].t0 = &t0;
+    start = stop;
+  }
+  int rc = 0, launched = 0;
+  for (int t = 0; t < n; ++t) {
+    jobs[t].ready = &ready;
+    jobs[t].abort = &abort;
+    jobs[t].nthreads = n;
+    if (pthread_create(&th[t], nullptr, local_worker, &jobs[t]) != 0) {
+      rc = -1;
+      abort.store(1);  // the started threads stop waiting for the missing ones
+      break;
+    }
+    ++launched;
+  }
+  double end = 0;
+  uint64_t bytes = 0;
+  for (int t = 0; t < launched; ++t) {
+    pthread_join(th[t], nullptr);
+    end = jobs[t].end > end ? jobs[t].end : end;
+    bytes += jobs[t].bytes;
+    if (jobs[t].err) rc = -1;
+  }
+  if (bytes_out) *bytes_out = bytes;
+  if (secs_out) *secs_out = end - t0.load();
+  return rc;
+}
