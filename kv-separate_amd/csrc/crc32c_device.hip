@@ -58,8 +58,9 @@ struct DevTables {
   uint32_t znarrow[4][256]; // Z_{16 kNarrowLanes}: the replicated table of the narrow kernel
   uint32_t zsmall[3][4][256];  // Z_16K, Z_32K, Z_64K: the automatic smaller pieces of small batches
   uint32_t x2n[64];         // x^(2^k) mod P (reflected): Z_n for ANY n by square-and-multiply (gf2_shift)
+  uint32_t xinv[16];        // x^(-8k) mod P: Z_k^-1, a register rewound over k bytes (the padded-head variant)
 };
-static_assert(sizeof(DevTables) == 4096 * 13 + 1024 + 256, "table layout");
+static_assert(sizeof(DevTables) == 4096 * 13 + 1024 + 256 + 64, "table layout");
 constexpr uint64_t kSmallPiece = 16 * 1024;  // zsmall[k] is Z_{kSmallPiece << k}
 
 struct PiecesArgs {
@@ -219,14 +220,16 @@ struct Staged {
 // kAlign: the rows end at ar = a1 rounded down to 128 B (never below h0), so every row is exactly eight 128-B
 // lines and no line is requested by two rows; the m < 8 whole 16-B chunks between ar and a1 are one extra load
 // (lanes 8-m .. 7) folded by a 3-level lane tree in finish().
-template <int kG, bool kNT, bool kAlign = false>
+// kPad (diag variant, exact): no serial head -- the body starts at the 16-B boundary at or below ps, the bytes before
+// ps are zeroed in that first chunk, and the item's register enters there already rewound over them (fill_set).
+template <int kG, bool kNT, bool kAlign = false, bool kPad = false>
 __device__ __forceinline__ void stage(Staged<kG>& s, uintptr_t ps, uintptr_t pe, uint32_t lane, uintptr_t dummy,
                                       uint32_t vz) {
   s.ps = ps;
   s.pe = pe;
   s.dummy = dummy;
   s.hbase = ps & ~uintptr_t(15);
-  s.h0 = (ps + 15) & ~uintptr_t(15);
+  s.h0 = kPad && ps < pe ? s.hbase : (ps + 15) & ~uintptr_t(15);
   if (s.h0 > pe) s.h0 = pe;
   s.a1 = pe & ~uintptr_t(15);
   if (s.a1 < s.h0) s.a1 = s.h0;
@@ -254,7 +257,18 @@ __device__ __forceinline__ void stage(Staged<kG>& s, uintptr_t ps, uintptr_t pe,
     s.A[i] = ld16<kNT>(last ? s.seg + (1 + i < last ? 1 + i : last) * kRowBytes : dummy);
 }
 
+// The 16-B chunk with its bytes [0, k) zeroed (k < 16).
+__device__ __forceinline__ uint4 mask_low(uint4 c, uint32_t k) {
+  auto m = [k](int d) -> uint32_t {
+    const int lo = int(k) - 4 * d;
+    return lo <= 0 ? ~0u : lo >= 4 ? 0u : (~0u << (8 * lo));
+  };
+  return make_uint4(c.x & m(0), c.y & m(1), c.z & m(2), c.w & m(3));
+}
+
 // Raw CRC register after consuming the staged item [ps, pe) from register `reg` (no final inversion).
+// kAbl == 6 (diag variant, exact): the padded head of stage<kPad>: `reg` is the register at hbase (rewound), the
+// first chunk's bytes before ps are zeroed here.
 // Rows beyond the staged ones stream kG at a time, the next kG in flight during compute.
 //
 // `next()` stages the FOLLOWING work item's loads.  It is called once, as late as possible while still ahead
@@ -270,7 +284,10 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     const uint64_t K = s.K, last = K - 1;
     if (kAbl != 3 && s.ps < s.h0) reg = serial16(lds, reg, uniform4(s.hc), int(s.ps - s.hbase), int(s.h0 - s.hbase));
     uint4 v = s.v_ok ? s.v : make_uint4(0, 0, 0, 0);
-    if (s.seg == s.h0) v.x ^= reg;  // the head register enters as pending word at h0
+    if (s.seg == s.h0) {  // the head register enters as pending word at h0
+      if (kAbl == 6) v = mask_low(v, uint32_t(s.ps - s.h0));
+      v.x ^= reg;
+    }
     uint32_t c0 = v.x, c1 = v.y, c2 = v.z, c3 = v.w;
 
 #define KVSEP_ROW(V)                                  \
@@ -371,7 +388,10 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     // per lane the STEP4W re-injection, then a 3-level tree over lanes 0..7 (Z_16, Z_32, Z_64): lane 7 ends with
     // the pending word at a1 - 4
     uint4 e = lane < 8 && lane + s.m >= 8 ? s.et : make_uint4(0, 0, 0, 0);
-    if (lane + s.m == 8) e.x ^= reg;
+    if (lane + s.m == 8) {
+      if (kAbl == 6 && !s.K) e = mask_low(e, uint32_t(s.ps - s.h0));  // the first chunk (ar == h0)
+      e.x ^= reg;
+    }
     uint32_t p = zmap_x(lds, kZ4Off, e.x, e.y);
     p = zmap_x(lds, kZ4Off, p, e.z);
     p = zmap_x(lds, kZ4Off, p, e.w);
@@ -389,7 +409,11 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     }
     reg = zmap(lds, kZ4Off, uint32_t(__builtin_amdgcn_readlane(int(p), 7)));  // register at a1
   }
-  if (kAbl != 3 && s.a1 < s.pe) reg = serial16(lds, reg, uniform4(s.tc), 0, int(s.pe - s.a1));
+  if (kAbl != 3 && s.a1 < s.pe) {
+    uint4 t = uniform4(s.tc);
+    if (kAbl == 6 && s.a1 == s.h0) t = mask_low(t, uint32_t(s.ps - s.h0));  // no body: the tail chunk is the first
+    reg = serial16(lds, reg, t, 0, int(s.pe - s.a1));
+  }
   return reg;
 }
 
@@ -751,6 +775,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
       w_pe = blk + re;
       w_b = uint32_t(b);
       w_reg0 = first ? ~(a.init ? a.init[b] : 0u) : 0u;
+      if (kAbl == 6 && w_ps < w_pe && (w_ps & 15u) && w_reg0)  // padded head: the register rewound to hbase
+        w_reg0 = gf2_mulmod(a.tabs->xinv[w_ps & 15u], w_reg0);
       w_only = only ? 1u : 0u;
       if (kVerify) w_exp = only ? a.expect[b] : 0u;  // travels with the descriptors, a window ahead of its use
     }
@@ -776,7 +802,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
     it.exp = kVerify ? rl(w_exp) : 0u;
     const uintptr_t ps = (uintptr_t(rl(uint32_t(w_ps >> 32))) << 32) | uintptr_t(rl(uint32_t(w_ps)));
     const uintptr_t pe = (uintptr_t(rl(uint32_t(w_pe >> 32))) << 32) | uintptr_t(rl(uint32_t(w_pe)));
-    stage<kG, kNT, kAlign>(st, ps, pe, lane, reinterpret_cast<uintptr_t>(a.tabs), vz);
+    stage<kG, kNT, kAlign, kAbl == 6>(st, ps, pe, lane, reinterpret_cast<uintptr_t>(a.tabs), vz);
   };
   auto emit = [&](const Item& it, uint32_t reg) {
     if (lane == 0) {
@@ -1620,6 +1646,7 @@ int upload_tables(kvsep_crc32c_ctx* c) {
   for (int k = 0; k < 3; ++k) gf2::byte_tables(gf2::zero_bytes_map(kSmallPiece << k), &h.zsmall[k][0][0]);
   gf2::byte_tables(gf2::zero_bytes_map(kNarrowRow), &h.znarrow[0][0]);
   gf2::x2n_table(h.x2n);
+  gf2::xinv_table(h.xinv);
   if (!c->d_tabs) KVSEP_HIP(hipMalloc(&c->d_tabs, sizeof(DevTables)));
   KVSEP_HIP(hipMemcpy(c->d_tabs, &h, sizeof(DevTables), hipMemcpyHostToDevice));
   return KVSEP_OK;

@@ -93,5 +93,19 @@ inline void x2n_table(uint32_t* out) {
   for (int k = 1; k < 64; ++k) out[k] = mulmod(out[k - 1], out[k - 1]);
 }
 
+// x^-1 mod P: P has constant term 1, so x * (P - 1)/x = P - 1 = 1 mod P.  In the reflected representation (P - 1)/x
+// is the constant without its x^0 bit (bit 31), every power moved down by one (bit 31 - i -> bit 32 - i: a left
+// shift) and x^31 (bit 0) from P's x^32.
+constexpr uint32_t kXInverse = (kPolyReflected << 1) | 1u;
+
+// out[k] = x^(-8k) mod P, k < 16: Z_k^-1, the register rewound over k zero bytes (a register entering k zero bytes
+// before position q that reaches R at q is Z_k^-1(R)).
+inline void xinv_table(uint32_t* out) {
+  uint32_t x8 = 0x80000000u;  // x^0
+  for (int i = 0; i < 8; ++i) x8 = mulmod(x8, kXInverse);
+  out[0] = 0x80000000u;
+  for (int k = 1; k < 16; ++k) out[k] = mulmod(out[k - 1], x8);
+}
+
 }  // namespace gf2
 }  // namespace kvsep

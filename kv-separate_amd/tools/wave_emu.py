@@ -1092,7 +1092,7 @@ TABLES_DUMP = r'''
 #include "gf2.h"
 using namespace kvsep;
 struct DevTables { uint32_t z1024[4][256], z4[4][256], ztree[6][4][256], byte1[256], zpiece[4][256], znarrow[4][256],
-                   zsmall[3][4][256], x2n[64]; };
+                   zsmall[3][4][256], x2n[64], xinv[16]; };
 int main() {
   static DevTables h;
   gf2::byte_tables(gf2::zero_bytes_map(1024), &h.z1024[0][0]);
@@ -1103,20 +1103,10 @@ int main() {
   for (int k = 0; k < 3; ++k) gf2::byte_tables(gf2::zero_bytes_map((16 * 1024ull) << k), &h.zsmall[k][0][0]);
   gf2::byte_tables(gf2::zero_bytes_map(128), &h.znarrow[0][0]);
   gf2::x2n_table(h.x2n);
+  gf2::xinv_table(h.xinv);
   fwrite(&h, sizeof h, 1, stdout);
 }
 '''
-
-
-def dev_tables() -> bytes:
-    """The DevTables image upload_tables (csrc/crc32c_device.hip) copies to the device, from the same gf2.h."""
-    with tempfile.TemporaryDirectory() as t:
-        src, exe = os.path.join(t, "d.cpp"), os.path.join(t, "d")
-        open(src, "w").write(DUMP)
-        subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", os.path.join(HERE, "..", "csrc"), src, "-o", exe])
-        img = subprocess.check_output([exe])
-    assert len(img) == 4096 * 13 + 1024 + 256
-    return img
 
 
 def dev_tables(csrc=os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "csrc")) -> bytes:
@@ -1126,5 +1116,5 @@ def dev_tables(csrc=os.path.join(os.path.dirname(os.path.abspath(__file__)), "..
         open(src, "w").write(TABLES_DUMP)
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", csrc, src, "-o", exe])
         img = subprocess.check_output([exe])
-    assert len(img) == 4096 * 13 + 1024 + 256
+    assert len(img) == 4096 * 13 + 1024 + 256 + 64
     return img
