@@ -220,8 +220,9 @@ struct Staged {
 // kAlign: the rows end at ar = a1 rounded down to 128 B (never below h0), so every row is exactly eight 128-B
 // lines and no line is requested by two rows; the m < 8 whole 16-B chunks between ar and a1 are one extra load
 // (lanes 8-m .. 7) folded by a 3-level lane tree in finish().
-// kPad (diag variant, exact): no serial head -- the body starts at the 16-B boundary at or below ps, the bytes before
-// ps are zeroed in that first chunk, and the item's register enters there already rewound over them (fill_set).
+// kPad (round 4, the shipped form): no serial head -- the body starts at the 16-B boundary at or below ps, the bytes
+// before ps are zeroed in that first chunk, and the item's register enters there already rewound over them
+// (x^-8k, fill_set).  A short item's head was a chain of up to 6 dependent LDS lookups ahead of its first fold.
 template <int kG, bool kNT, bool kAlign = false, bool kPad = false>
 __device__ __forceinline__ void stage(Staged<kG>& s, uintptr_t ps, uintptr_t pe, uint32_t lane, uintptr_t dummy,
                                       uint32_t vz) {
@@ -267,8 +268,8 @@ __device__ __forceinline__ uint4 mask_low(uint4 c, uint32_t k) {
 }
 
 // Raw CRC register after consuming the staged item [ps, pe) from register `reg` (no final inversion).
-// kAbl == 6 (diag variant, exact): the padded head of stage<kPad>: `reg` is the register at hbase (rewound), the
-// first chunk's bytes before ps are zeroed here.
+// kPad: the padded head of stage<kPad>: `reg` is the register at hbase (rewound), the first chunk's bytes before ps
+// are zeroed here.
 // Rows beyond the staged ones stream kG at a time, the next kG in flight during compute.
 //
 // `next()` stages the FOLLOWING work item's loads.  It is called once, as late as possible while still ahead
@@ -277,7 +278,8 @@ __device__ __forceinline__ uint4 mask_low(uint4 c, uint32_t k) {
 // lets the compiler keep all 16 LDS lookups of a row in flight instead of 2 -- and (b) the next item's
 // loads are the most recent ones, so every wait of this item stays a counted vmcnt that leaves them in
 // flight across the lane merge.
-template <int kG, bool kNT, int kAbl = 0, bool kAlign = false, typename Next>  // kAbl != 0: ablations (wrong)
+template <int kG, bool kNT, int kAbl = 0, bool kAlign = false, bool kPad = false,
+          typename Next>  // kAbl != 0: ablations (wrong)
 __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, uint32_t reg, uint32_t lane,
                                            uint32_t lc0, uint32_t lc1, Next&& next) {
   if (s.K) {
@@ -285,7 +287,7 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     if (kAbl != 3 && s.ps < s.h0) reg = serial16(lds, reg, uniform4(s.hc), int(s.ps - s.hbase), int(s.h0 - s.hbase));
     uint4 v = s.v_ok ? s.v : make_uint4(0, 0, 0, 0);
     if (s.seg == s.h0) {  // the head register enters as pending word at h0
-      if (kAbl == 6) v = mask_low(v, uint32_t(s.ps - s.h0));
+      if (kPad) v = mask_low(v, uint32_t(s.ps - s.h0));
       v.x ^= reg;
     }
     uint32_t c0 = v.x, c1 = v.y, c2 = v.z, c3 = v.w;
@@ -389,7 +391,7 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     // the pending word at a1 - 4
     uint4 e = lane < 8 && lane + s.m >= 8 ? s.et : make_uint4(0, 0, 0, 0);
     if (lane + s.m == 8) {
-      if (kAbl == 6 && !s.K) e = mask_low(e, uint32_t(s.ps - s.h0));  // the first chunk (ar == h0)
+      if (kPad && !s.K) e = mask_low(e, uint32_t(s.ps - s.h0));  // the first chunk (ar == h0)
       e.x ^= reg;
     }
     uint32_t p = zmap_x(lds, kZ4Off, e.x, e.y);
@@ -411,7 +413,7 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
   }
   if (kAbl != 3 && s.a1 < s.pe) {
     uint4 t = uniform4(s.tc);
-    if (kAbl == 6 && s.a1 == s.h0) t = mask_low(t, uint32_t(s.ps - s.h0));  // no body: the tail chunk is the first
+    if (kPad && s.a1 == s.h0) t = mask_low(t, uint32_t(s.ps - s.h0));  // no body: the tail chunk is the first
     reg = serial16(lds, reg, t, 0, int(s.pe - s.a1));
   }
   return reg;
@@ -677,6 +679,10 @@ template <bool kPlanned, bool kDynamic, int kG, bool kNT, bool kAhead, int kAbl 
           bool kAlign = true, bool kVerify = false>
 __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
+  // the padded head (stage<kPad>); diag variant 26 (kAbl == 6) keeps the serial head of rounds 1-3 for A/B: measured
+  // 3a -0.8 / -1.8 %, config 4 -0.1 / -0.2 %, 3b and config 4's short blocks equal, in one process on two boxes
+  // (profiles/round4/pad_variant/)
+  constexpr bool kPad = kAbl != 6;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   const uint32_t tid = threadIdx.x;
   KVSEP_WSTAMP_ENTRY();  // stamp hooks (crc32c_hooks.inc): empty in the shipped library
@@ -775,7 +781,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
       w_pe = blk + re;
       w_b = uint32_t(b);
       w_reg0 = first ? ~(a.init ? a.init[b] : 0u) : 0u;
-      if (kAbl == 6 && w_ps < w_pe && (w_ps & 15u) && w_reg0)  // padded head: the register rewound to hbase
+      if (kPad && w_ps < w_pe && (w_ps & 15u) && w_reg0)  // padded head: the register rewound to hbase
         w_reg0 = gf2_mulmod(a.tabs->xinv[w_ps & 15u], w_reg0);
       w_only = only ? 1u : 0u;
       if (kVerify) w_exp = only ? a.expect[b] : 0u;  // travels with the descriptors, a window ahead of its use
@@ -802,7 +808,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
     it.exp = kVerify ? rl(w_exp) : 0u;
     const uintptr_t ps = (uintptr_t(rl(uint32_t(w_ps >> 32))) << 32) | uintptr_t(rl(uint32_t(w_ps)));
     const uintptr_t pe = (uintptr_t(rl(uint32_t(w_pe >> 32))) << 32) | uintptr_t(rl(uint32_t(w_pe)));
-    stage<kG, kNT, kAlign, kAbl == 6>(st, ps, pe, lane, reinterpret_cast<uintptr_t>(a.tabs), vz);
+    stage<kG, kNT, kAlign, kPad>(st, ps, pe, lane, reinterpret_cast<uintptr_t>(a.tabs), vz);
   };
   auto emit = [&](const Item& it, uint32_t reg) {
     if (lane == 0) {
@@ -823,7 +829,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
     // The next item's HBM loads overlap the end of this item's compute (finish() stages them late, see
     // there).  The take is unconditional (the last item re-stages itself): on a path without it, this item's loads would be the most recent ones and the
     // compiler's counted wait (which merges both paths) would drain everything, vmcnt(0), on every item.
-    emit(ia, finish<kG, kNT, kAbl, kAlign>(lds, A, ia.reg0, lane, lc0, lc1, [&]() {
+    emit(ia, finish<kG, kNT, kAbl, kAlign, kPad>(lds, A, ia.reg0, lane, lc0, lc1, [&]() {
            if (kAhead) take(hn ? g + 1 : g, ib, B);
          }));
     KVSEP_WSTAMP_ITEM_END(ia);
