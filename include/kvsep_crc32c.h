@@ -78,7 +78,9 @@ int kvsep_crc32c_ctx_set_piece_bytes(kvsep_crc32c_ctx* ctx, uint64_t piece_bytes
 int kvsep_crc32c_ctx_set_schedule(kvsep_crc32c_ctx* ctx, int dynamic);
 /* Kernel of unsplit batches: 0 = auto (default; the narrow kernel for many blocks <= 8-32 KiB, its sorted-window
  * form when the batch is ragged: max_len > 1.25 x total_bytes / count), 1 = always the wide kernel, 2 = the narrow
- * kernel whenever max_len <= 64 KiB, 3 / 4 = as 2 with 16- / 8-wave workgroups, 5 = as 2 in the sorted-window form.
+ * kernel whenever max_len <= 64 KiB, 3 / 4 = as 2 with 16- / 8-wave workgroups, 5 = as 2 in the sorted-window form,
+ * 6 = as 2 with each workgroup's contiguous run of groups dealt to its waves by an LDS claim counter (round 4; auto
+ * takes it for uniform batches of up to 256 Ki blocks <= 8 KiB).
  * A choice of speed only: every kernel is exact for every block.  No environment variable changes it. */
 int kvsep_crc32c_ctx_set_kernel(kvsep_crc32c_ctx* ctx, int kernel);
 /* Pre-size scratch so later calls of up to `count` blocks / `total_bytes` bytes do not allocate
@@ -88,7 +90,8 @@ int kvsep_crc32c_reserve(kvsep_crc32c_ctx* ctx, uint64_t count, uint64_t total_b
 int kvsep_crc32c_ctx_set_timing(kvsep_crc32c_ctx* ctx, int enable);
 int kvsep_crc32c_ctx_get_timing(kvsep_crc32c_ctx* ctx, double* total_ms, uint64_t* launches); /* syncs + resets */
 /* Name of the main kernel a batch of `count` blocks with these total_bytes / max_len hints runs on
- * ("crc32c_pieces_kernel", "crc32c_narrow_kernel" or "crc32c_narrow_sorted_kernel"): the kernel the timing above
+ * ("crc32c_pieces_kernel", "crc32c_narrow_kernel", "crc32c_narrow_claim_kernel" or "crc32c_narrow_sorted_kernel"):
+ * the kernel the timing above
  * and a rocprofv3 trace refer to. */
 const char* kvsep_crc32c_kernel_name(kvsep_crc32c_ctx* ctx, uint64_t count, uint64_t total_bytes, uint64_t max_len);
 

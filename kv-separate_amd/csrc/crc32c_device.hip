@@ -1267,6 +1267,131 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   if (kVerify) verify_publish(a, wave);
 }
 
+// Batches of short blocks up to ~1 GiB (narrow_form 10, round 4): the workgroup owns a contiguous run of 8-block
+// groups and deals it to its 8 waves through an LDS claim counter (one ds_add per group: lgkmcnt, never in the rows'
+// vmcnt stream), so the waves the memory system serves first take more of the run.  Otherwise the narrow kernel's
+// pipeline: a group's rows are staged inside the previous group's finish, and the group after that is claimed and its
+// descriptors loaded right after the previous group's emit.  Measured against the shipped forms in one process
+// (tools/narrow_variants_probe.py, 4 KiB blocks, graph replay; profiles/round4/queue_variants/): 128 MiB 26.1 vs 28.2
+// us, 256 MiB (config 2) 45.3 vs 48.4, 512 MiB 82.5 vs 90.5, 1 GiB 154.6 vs 165.3 -- but 2 GiB 346.8 vs 313.8 and 4 GiB
+// 641.8 vs 622.1 (the wave-major runs of the 8-wave narrow kernel stream better there).  The same run dealt round-robin
+// with no claims measured within 1 % of the claims: most of the gain is the workgroup-contiguous run itself.  Blocks
+// over the hint go to narrow_deferred right after their group (8 waves have the VGPRs for it inline).
+// kVerify: the verify form (stored words loaded before each group's remaining rows, verify_wave, verify_publish).
+template <int kG, int kThreads, bool kVerify = false>
+__global__ void __launch_bounds__(kThreads) crc32c_narrow_claim_kernel(PiecesArgs a) {
+  constexpr uint32_t kWaves = kThreads / 64, kPerGroup = 64 / kNarrowLanes, kNone = 0xffffffffu;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+  __shared__ uint32_t claimed;  // groups of the run claimed after each wave's first (static) one
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63u;
+  const uint32_t j = lane & (kNarrowLanes - 1);
+  const uint32_t slot = lane / kNarrowLanes;
+  const uint32_t lc0 = LdsFull::lc0(lane), lc1 = LdsFull::lc1(lane);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uintptr_t dummy = reinterpret_cast<uintptr_t>(a.tabs);
+  const uint64_t count = a.count;
+  const uint32_t hint32 = uint32_t(a.hint);  // <= 64 KiB (use_narrow)
+  // this workgroup's contiguous run of groups [run0, run1); group indices fit 32 bits (count < 2^32)
+  const uint32_t groups = uint32_t((count + kPerGroup - 1) / kPerGroup);
+  const uint32_t per_wg = (groups + gridDim.x - 1) / gridDim.x;
+  const uint32_t run0 = blockIdx.x * per_wg < groups ? blockIdx.x * per_wg : groups;
+  const uint32_t run1 = run0 + per_wg < groups ? run0 + per_wg : groups;
+  if (tid == 0) claimed = 0;  // before the fill's barrier; every claim comes after it
+
+  bool ended = false;
+  auto next_group = [&]() -> uint32_t {  // claims only after the barrier; none once the run is used up
+    if (ended) return kNone;
+    uint32_t c = 0;
+    if (lane == 0) c = atomicAdd(&claimed, 1u);
+    c = uint32_t(__builtin_amdgcn_readfirstlane(int(c)));
+    const uint32_t g = run0 + kWaves + c;
+    ended = g >= run1;
+    return ended ? kNone : g;
+  };
+  struct Desc {
+    uint64_t off;
+    uint32_t len, lenhi, init;
+  };
+  auto load_desc = [&](uint32_t g, Desc& d) {  // past the batch: loads stay in bounds, take() empties the slot
+    uint32_t sl = slot;
+    asm volatile("" : "+v"(sl));  // see load_desc in crc32c_narrow_kernel
+    const uint64_t blk = uint64_t(g) * kPerGroup + sl;
+    const bool in = g != kNone && blk < count;
+    const uint64_t bb = in ? blk : 0;
+    d.off = a.off[bb];
+    const uint2 l = *reinterpret_cast<const uint2*>(a.len + bb);
+    d.len = l.x;
+    d.lenhi = l.y;
+    d.init = *(a.init && in ? a.init + bb : &a.tabs->z4[0][0]);  // no init: a word that is 0 (Z_4 of byte 0)
+  };
+  struct CItem {
+    uint32_t g, reg0, kmin, kmax;
+    bool over, deferred;
+  };
+  Desc dn;
+  auto take = [&](uint32_t g, CItem& it, NStaged<kG>& st) {
+    const uint64_t blk = uint64_t(g) * kPerGroup + slot;
+    const bool in = g != kNone && blk < count;
+    const bool over = in && (dn.lenhi != 0 || dn.len > hint32);
+    it.deferred = __builtin_amdgcn_ballot_w64(over) != 0;
+    const bool live = in && !over;
+    it.g = g;
+    it.over = over;
+    it.reg0 = ~dn.init;
+    nstage<kG, true, true>(st, live ? reinterpret_cast<uintptr_t>(a.base) + dn.off : dummy, live ? dn.len : 0u, j,
+                           dummy);
+    uint32_t km = 0, kn = ~0u;
+#pragma unroll
+    for (uint32_t k = 0; k < kPerGroup; ++k) {
+      const uint32_t kk = uint32_t(__builtin_amdgcn_readlane(int(st.K), int(k * kNarrowLanes)));
+      km = km > kk ? km : kk;
+      kn = kn < kk ? kn : kk;
+    }
+    it.kmax = km;
+    it.kmin = kn;
+  };
+  uint32_t gn = kNone;  // the group staged next (its descriptors are in dn until its take)
+  auto step = [&](CItem& ia, NStaged<kG>& A, CItem& ib, NStaged<kG>& B) -> bool {
+    const uint64_t g0 = uint64_t(ia.g) * kPerGroup;
+    uint32_t ex = 0;
+    if (kVerify) {  // this group's stored words, before its remaining rows (see crc32c_narrow_kernel's step)
+      const uint64_t last = count - 1 - g0;
+      ex = ld32(a.expect + g0 + (slot < last ? slot : uint32_t(last)));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const uint32_t reg = nfinish<kG, true, 0, true>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
+                                                    [&]() { take(gn, ib, B); });
+    const bool mine = j == kNarrowLanes - 1 && g0 + slot < count && !ia.over;
+    if (kVerify) verify_wave(a, lane, mine, g0, slot, ~reg, ex);  // before the store
+    if (mine) emit_block(a, g0 + slot, ~reg);
+    if (ia.deferred)  // wave-uniform: this group's blocks over the hint, whole
+      narrow_deferred<kG, true, true, LdsFull, kVerify>(a, lds, g0, g0 + kPerGroup < count ? g0 + kPerGroup : count,
+                                                        dummy);
+    gn = next_group();  // the group after ib: claimed now, its descriptors loaded while ib runs
+    load_desc(gn, dn);
+    return ib.g != kNone;
+  };
+
+  // the wave's first group is static (the wave's slot of the run), its descriptors fetched during the LDS fill
+  uint32_t g0 = run0 + wave < run1 ? run0 + wave : kNone;
+  load_desc(g0, dn);
+  fill_lds<kThreads, true>(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
+  __syncthreads();
+  if (g0 != kNone) {
+    CItem cur, nxt;
+    NStaged<kG> S, T;
+    take(g0, cur, S);
+    gn = next_group();
+    load_desc(gn, dn);
+    for (;;) {
+      if (!step(cur, S, nxt, T)) break;
+      if (!step(nxt, T, cur, S)) break;
+    }
+  }
+  if (kVerify) verify_publish(a, wave);
+}
+
 // Bitonic sort of one (key, idx) pair per lane over the wavefront, ascending by key (ties by idx, so the two
 // lanes of every compare-exchange agree): 21 ds_bpermute stages of two values each.
 __device__ __forceinline__ void wave_sort64(uint32_t& key, uint32_t& idx, uint32_t lane) {
@@ -1605,7 +1730,7 @@ struct kvsep_crc32c_ctx {
   uint64_t piece_bytes = 128 * 1024;  // best of 32 KiB .. 1 MiB on configs 3a/3b/4
   bool piece_auto = true;             // smaller pieces for small batches (piece_for); off once set explicitly
   int dynamic = -1;  // -1 auto, 0 static, 1 guided
-  int kernel = 0;    // kvsep_crc32c_ctx_set_kernel: 0 auto (use_narrow), 1 wide only, 2-5 narrow when the hint allows
+  int kernel = 0;    // kvsep_crc32c_ctx_set_kernel: 0 auto (use_narrow), 1 wide only, 2-6 narrow when the hint allows
   uint32_t static_contig = 1;  // static schedule: contiguous runs (1) or round-robin items (0, set_schedule(2))
   int variant = 1;   // KVSEP_DIAG builds only: A/B and ablation variants of the wide kernel (launch_pieces_v)
   int narrow = 1;    // KVSEP_DIAG builds only: narrow-kernel variants
@@ -1756,11 +1881,13 @@ bool ragged_batch(uint64_t count, uint64_t total_bytes, uint64_t max_len) {
 }
 
 // Narrow-kernel form of a batch that use_narrow() put on the narrow kernels: 6 = 16-wave workgroups, 9 = 8-wave
-// workgroups (fill overlapped with the first loads), 20 = sorted windows (crc32c_narrow_sorted_kernel, 16 waves).
+// workgroups (fill overlapped with the first loads), 10 = workgroup-contiguous runs dealt by LDS claims
+// (crc32c_narrow_claim_kernel, 8 waves), 20 = sorted windows (crc32c_narrow_sorted_kernel, 16 waves).
 int narrow_form(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes, uint64_t max_len) {
   if (c->kernel == 3) return 6;
   if (c->kernel == 4) return 9;
   if (c->kernel == 5) return 20;
+  if (c->kernel == 6) return 10;
   // 16-wave workgroups below 128 Ki blocks of <= 8 KiB (32 Ki blocks of 8-32 KiB), 8-wave ones from there on.  A
   // small batch gives each wave only a couple of 8-block groups, and more waves hide more of the launch/first-load
   // ramp (256 MiB of 4 KiB blocks: 16 waves +2-5 %); a large one streams better with 8 (1 GiB of 4 KiB blocks:
@@ -1770,6 +1897,10 @@ int narrow_form(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes,
   // sorting 64-block windows by length makes the groups even (config 4's 902 K blocks <= 32 KiB: 0.93 -> 0.57 ms
   // against the 16-wave narrow kernel, 1.24 ms on the 8-wave one).
   if (ragged_batch(count, total_bytes, max_len)) return 20;
+  // Uniform blocks of <= 8 KiB up to 256 Ki of them (1 GiB of 4 KiB blocks): the claim kernel, 5-9 % faster than
+  // either form above from 128 MiB to 1 GiB of 4 KiB blocks; from 2 GiB on the wave-major 8-wave kernel streams
+  // better (crc32c_narrow_claim_kernel).
+  if (max_len <= 8 * 1024 && count < (1u << 18)) return 10;
   const bool eight_waves = max_len <= 8 * 1024 ? count >= (1u << 17) : count >= (1u << 15);
   return eight_waves ? 9 : 6;
 }
@@ -1948,9 +2079,10 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     int nv = narrow_form(c, count, total_bytes, max_len);
     nv = diag_narrow_form(c, nv);  // KVSEP_DIAG build only
     a.hint = max_len;
-    if (expect && (nv == 6 || nv == 9 || nv == 20)) {  // the verify form of the shipped narrow forms
+    if (expect && (nv == 6 || nv == 9 || nv == 10 || nv == 20)) {  // the verify form of the shipped narrow forms
       switch (nv) {
         case 9: crc32c_narrow_kernel<4, true, 512, true, 0, true, LdsFull, true><<<grid, 512, 0, s>>>(a); break;
+        case 10: crc32c_narrow_claim_kernel<4, 512, true><<<grid, 512, 0, s>>>(a); break;
         case 20: crc32c_narrow_sorted_kernel<4, true, 1024, false, 0, true><<<grid, 1024, 0, s>>>(a); break;
         default: crc32c_narrow_kernel<4, true, 1024, false, 0, true, LdsFull, true><<<grid, 1024, 0, s>>>(a); break;
       }
@@ -1965,6 +2097,7 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     if (!diag_launch_narrow(nv, grid, s, a, count))  // KVSEP_DIAG build only
     switch (nv) {
       case 9: crc32c_narrow_kernel<4, true, 512, true><<<grid, 512, 0, s>>>(a); break;
+      case 10: crc32c_narrow_claim_kernel<4, 512><<<grid, 512, 0, s>>>(a); break;
       case 20: crc32c_narrow_sorted_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
       default: crc32c_narrow_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
     }
@@ -2084,7 +2217,7 @@ int kvsep_crc32c_ctx_set_schedule(kvsep_crc32c_ctx* c, int dynamic) {
 }
 
 int kvsep_crc32c_ctx_set_kernel(kvsep_crc32c_ctx* c, int kernel) {
-  if (!c || kernel < 0 || kernel > 5) return set_err(KVSEP_EINVAL, "kernel must be 0..5");
+  if (!c || kernel < 0 || kernel > 6) return set_err(KVSEP_EINVAL, "kernel must be 0..6");
   std::lock_guard<std::mutex> g(c->mu);
   c->kernel = kernel;
   return KVSEP_OK;
@@ -2219,7 +2352,8 @@ const char* kvsep_crc32c_kernel_name(kvsep_crc32c_ctx* c, uint64_t count, uint64
   if (!c) return "";
   const bool planned = !(max_len != 0 && max_len <= c->piece_bytes);
   if (planned || !use_narrow(c, count, max_len)) return "crc32c_pieces_kernel";
-  return narrow_form(c, count, total_bytes, max_len) == 20 ? "crc32c_narrow_sorted_kernel" : "crc32c_narrow_kernel";
+  const int nf = narrow_form(c, count, total_bytes, max_len);
+  return nf == 20 ? "crc32c_narrow_sorted_kernel" : nf == 10 ? "crc32c_narrow_claim_kernel" : "crc32c_narrow_kernel";
 }
 
 int kvsep_stream_read_device(kvsep_crc32c_ctx* c, void* stream, const void* src, uint64_t nbytes, uint32_t* sink) {

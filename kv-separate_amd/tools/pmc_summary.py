@@ -15,7 +15,7 @@ import json
 import os
 import statistics
 
-CRC_KERNELS = ("crc32c_pieces_kernel", "crc32c_narrow_kernel")
+CRC_KERNELS = ("crc32c_pieces_kernel", "crc32c_narrow_kernel", "crc32c_narrow_claim_kernel", "crc32c_narrow_sorted_kernel")
 
 
 def per_launch(path, counter):

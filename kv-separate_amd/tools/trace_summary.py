@@ -14,7 +14,7 @@ import csv
 import json
 import statistics
 
-CRC_KERNELS = ("crc32c_pieces_kernel", "crc32c_narrow_kernel")
+CRC_KERNELS = ("crc32c_pieces_kernel", "crc32c_narrow_kernel", "crc32c_narrow_claim_kernel", "crc32c_narrow_sorted_kernel")
 
 
 def main():

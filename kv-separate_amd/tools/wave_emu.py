@@ -653,6 +653,19 @@ class Workgroup:
                 self.lds[ad:ad + 4 * n] = np.frombuffer(
                     struct.pack('<%dI' % n, *[int(w.v[first + i][l]) for i in range(n)]), dtype=np.uint8)
             return
+        if op in ('ds_add_rtn_u32', 'ds_add_u32'):  # LDS atomic add; active lanes in lane order
+            ret = op == 'ds_add_rtn_u32'
+            a = w.vget(o[1] if ret else o[0]).astype(np.int64) + off
+            data = w.vget(o[2] if ret else o[1])
+            old_vals = np.zeros(64, dtype=np.uint32)
+            for l in np.nonzero(act)[0]:
+                ad = int(a[l])
+                cur = struct.unpack('<I', self.lds[ad:ad + 4].tobytes())[0]
+                old_vals[l] = cur
+                self.lds[ad:ad + 4] = np.frombuffer(struct.pack('<I', (cur + int(data[l])) & M32), dtype=np.uint8)
+            if ret:
+                w.vset(o[0], old_vals)
+            return
         if op == 'ds_bpermute_b32':
             addr = w.vget(o[1]).astype(np.int64) + off
             data = w.vget(o[2])
@@ -986,11 +999,24 @@ def kernel_code(asm: str, name: str):
     return _FN_CACHE[key]
 
 
+def group_segment_bytes(asm: str, name: str) -> int:
+    """The kernel's LDS size from its .amdhsa_kernel descriptor in the assembly (0 if not found)."""
+    key = ("lds", asm, name, os.path.getmtime(asm))
+    if key not in _FN_CACHE:
+        text = open(asm).read()
+        m = re.search(r"\.amdhsa_kernel " + re.escape(name) + r"\s.*?\.amdhsa_group_segment_fixed_size (\d+)", text,
+                      re.S)
+        _FN_CACHE[key] = int(m.group(1)) if m else 0
+    return _FN_CACHE[key]
+
+
 def launch(mem: Memory, asm: str, name: str, threads: int, lds_bytes: int, fields: dict, grid: int, wgs=None) -> int:
     """Run workgroups `wgs` (default: the whole grid, one after another) of a PiecesArgs kernel; returns the number of
     wave-instructions executed.  Workgroups run to completion in order, so a dynamic (atomic-counter) schedule hands
-    every item to the first workgroup -- functionally the same result, a different interleaving."""
+    every item to the first workgroup -- functionally the same result, a different interleaving.  The LDS is at least
+    the kernel's own group segment size."""
     insns, labels = kernel_code(asm, name)
+    lds_bytes = max(lds_bytes, group_segment_bytes(asm, name))
     d_ka = mem.alloc(ARGS_BYTES + 256, data=pieces_kernarg(fields, grid, threads))
     steps = 0
     for g in (range(grid) if wgs is None else wgs):

@@ -38,7 +38,7 @@ def test_capture_and_replay(layout, oracle):
     try:
         ctx.reserve(off.size, int(ln.sum()))
         assert ctx.kernel_name(off.size, int(ln.max())) == (
-            "crc32c_pieces_kernel" if layout == "planned" else "crc32c_narrow_kernel")
+            "crc32c_pieces_kernel" if layout == "planned" else "crc32c_narrow_claim_kernel")  # 20,000 x 4 KiB
         kvsep.fill_splitmix64(data.data_ptr(), span, 1, 0)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
@@ -54,13 +54,13 @@ def test_capture_and_replay(layout, oracle):
         ctx.close()
 
 
-@pytest.mark.parametrize("layout", ["planned", "unplanned", "narrow", "sorted"])
+@pytest.mark.parametrize("layout", ["planned", "unplanned", "narrow", "sorted", "claim"])
 def test_capture_verify_form(layout, oracle):
     """The verify form captured once and replayed: its verdict words are published by the last workgroup of the
     publishing kernel (the CRC kernel; the combine kernel for a split batch), which also resets the context's
     accumulators, so a verdict never leaks into the next replay: clean -> one bad record -> three bad records spread
     over the batch (several workgroups post) -> clean again, each replayed twice, two calls per replay."""
-    kernel = {"planned": "auto", "unplanned": "wide", "narrow": "narrow16", "sorted": "sorted"}[layout]
+    kernel = {"planned": "auto", "unplanned": "wide", "narrow": "narrow16", "sorted": "sorted", "claim": "claim"}[layout]
     if layout == "planned":
         off, ln = W.cfg3_layout(vlog=True, count=40)  # split blocks: the combine kernel publishes
         hint = 0

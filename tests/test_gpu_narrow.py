@@ -145,13 +145,15 @@ def test_sorted_windows_ragged(oracle, pool, count):
         ctx.set_kernel("auto")
         n = 40000  # enough blocks for the narrow kernels (use_narrow); ragged -> sorted, uniform -> plain
         assert ctx.kernel_name(n, 32768, n * 2000) == "crc32c_narrow_sorted_kernel"
-        assert ctx.kernel_name(n, 4096, n * 4096) == "crc32c_narrow_kernel"
-        assert ctx.kernel_name(n, 4096) == "crc32c_narrow_kernel"  # total_bytes unknown: not ragged
+        assert ctx.kernel_name(n, 4096, n * 4096) == "crc32c_narrow_claim_kernel"  # uniform, < 256 Ki blocks
+        assert ctx.kernel_name(n, 4096) == "crc32c_narrow_claim_kernel"  # total_bytes unknown: not ragged
+        assert ctx.kernel_name(1 << 18, 4096, (1 << 18) * 4096) == "crc32c_narrow_kernel"  # 1 GiB and up: 8-wave
+        assert ctx.kernel_name(n, 16384, n * 16384) == "crc32c_narrow_kernel"  # blocks over 8 KiB
     finally:
         ctx.close()
 
 
-@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted"])
+@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted", "claim"])
 @pytest.mark.parametrize("count", [70000, 200000])
 def test_verify_several_groups_per_wave(oracle, pool, kernel, count):
     """Verify form with several 8-block groups per wave (3 and 7 per 64-block window at these counts): the sorted
@@ -182,7 +184,7 @@ def test_verify_several_groups_per_wave(oracle, pool, kernel, count):
         ctx.close()
 
 
-@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted"])
+@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted", "claim"])
 def test_every_end_geometry(oracle, pool, kernel):
     """Every case of the slot's end path: m = 0..7 whole 16-B chunks between the 128-B grid and the 16-B end (m = 7
     uses all of lanes 0..6 of the tail load), each with head and tail bytes 0..15, with and without body rows."""
@@ -208,7 +210,7 @@ def test_every_end_geometry(oracle, pool, kernel):
     assert np.array_equal(got, oracle.batch(data, off, ln, init))
 
 
-@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted"])
+@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted", "claim"])
 def test_verify_mismatch_on_deferred_block(oracle, pool, kernel):
     """Verify form under an understated max_len: blocks longer than the hint leave their 8-block group and
     are checksummed by the deferred walk, whose compare is verify_uniform over the wave-uniform stored word.  Mismatches
