@@ -724,7 +724,8 @@ def main():
                    "single_thread_GiBps": round(res[1][0], 3),
                    "nproc": os.cpu_count(), "affinity_cores": aff, "cpu_model": cpu_model(),
                    "cgroup_cpu_max": quota_raw, "cgroup_cpu_limit": quota,
-                   "numa_nodes": {str(n): f"{len(c)} cpus ({c[0]}-{c[-1]})" for n, c in nodes.items() if c},
+                   "numa_nodes": {str(n): _read(f"/sys/devices/system/node/node{n}/cpulist") or f"{len(c)} cpus"
+                                  for n, c in nodes.items() if c},
                    "limit_note": (f"this process may use {quota:g} CPUs' worth of time (cgroup cpu.max) of the {aff} "
                                   f"it may run on: rates flatten from {int(quota)} threads on" if quota and quota < aff
                                   else "no cgroup CPU limit below the affinity set")}
