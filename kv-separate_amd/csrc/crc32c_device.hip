@@ -1897,10 +1897,13 @@ int narrow_form(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes,
   // sorting 64-block windows by length makes the groups even (config 4's 902 K blocks <= 32 KiB: 0.93 -> 0.57 ms
   // against the 16-wave narrow kernel, 1.24 ms on the 8-wave one).
   if (ragged_batch(count, total_bytes, max_len)) return 20;
-  // Uniform blocks of <= 8 KiB up to 256 Ki of them (1 GiB of 4 KiB blocks): the claim kernel, 5-9 % faster than
-  // either form above from 128 MiB to 1 GiB of 4 KiB blocks; from 2 GiB on the wave-major 8-wave kernel streams
-  // better (crc32c_narrow_claim_kernel).
-  if (max_len <= 8 * 1024 && count < (1u << 18)) return 10;
+  // The claim kernel (crc32c_narrow_claim_kernel) for uniform blocks of <= 8 KiB from 32 Ki of them up to 384 Ki of
+  // <= 4 KiB (128 MiB - 1.5 GiB of 4 KiB blocks) or 64 Ki of 4-8 KiB.  Measured against both forms below in one
+  // process (profiles/round4/queue_variants/claim_*.log, graph replay): 4 KiB blocks 128 MiB 26.8 vs 27.8 us, 256 MiB
+  // 45.9 vs 48.3, 512 MiB 83.1 vs 91.0, 1 GiB 156.7 vs 166.6, 1.5 GiB 241.4 vs 252.9, but 2 GiB 347.6 vs 314.0 (the
+  // wave-major 8-wave kernel streams better from there); 2 KiB blocks 256 MiB 44.9 vs 47.6, 1 GiB 165.1 vs 163.8;
+  // 8 KiB blocks 256 MiB 45.2 vs 45.8, 1 GiB 156.9 vs 155.0; 16 KiB blocks never (256 MiB 50.1 vs 44.0).
+  if (max_len <= 8 * 1024 && count >= (1u << 15) && count <= (max_len <= 4 * 1024 ? 3u << 17 : 1u << 16)) return 10;
   const bool eight_waves = max_len <= 8 * 1024 ? count >= (1u << 17) : count >= (1u << 15);
   return eight_waves ? 9 : 6;
 }

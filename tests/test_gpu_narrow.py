@@ -147,7 +147,8 @@ def test_sorted_windows_ragged(oracle, pool, count):
         assert ctx.kernel_name(n, 32768, n * 2000) == "crc32c_narrow_sorted_kernel"
         assert ctx.kernel_name(n, 4096, n * 4096) == "crc32c_narrow_claim_kernel"  # uniform, < 256 Ki blocks
         assert ctx.kernel_name(n, 4096) == "crc32c_narrow_claim_kernel"  # total_bytes unknown: not ragged
-        assert ctx.kernel_name(1 << 18, 4096, (1 << 18) * 4096) == "crc32c_narrow_kernel"  # 1 GiB and up: 8-wave
+        assert ctx.kernel_name(3 << 17, 4096, (3 << 17) * 4096) == "crc32c_narrow_claim_kernel"  # 1.5 GiB
+        assert ctx.kernel_name(1 << 19, 4096, (1 << 19) * 4096) == "crc32c_narrow_kernel"  # 2 GiB and up: 8-wave
         assert ctx.kernel_name(n, 16384, n * 16384) == "crc32c_narrow_kernel"  # blocks over 8 KiB
     finally:
         ctx.close()
