@@ -696,6 +696,7 @@ def main():
         oracle = load_oracle()
         parity = check_results([Plan(args.config, world, r) for r in range(world)], results, oracle)
         parity["all_blocks_match"] = parity["mismatches"] == 0 and parity["mismatching_digest_ranges"] == 0
+        res = None
         if not args.no_cpu and world == 1:
             aff = len(os.sched_getaffinity(0))
             most = args.cpu_threads or aff
@@ -705,7 +706,13 @@ def main():
                 counts.add(max(1, int(quota)))  # the cgroup's CPU share: the scaling must flatten there
             counts = sorted(counts)
             nsample = min(args.cpu_sample_blocks, count)
-            res, host, hoff, lens, idx, kind = cpu_baseline(oracle, data, off, ln, nsample, counts, args.cpu_seconds)
+            try:
+                res, host, hoff, lens, idx, kind = cpu_baseline(oracle, data, off, ln, nsample, counts,
+                                                                args.cpu_seconds)
+            except Exception as e:  # the headline line never depends on the CPU leg
+                log(f"[rank 0] cpu baseline failed: {e}")
+                res = None
+        if res is not None:
             threads = max(counts, key=lambda t: res[t][0])  # the baseline is the CPU's best thread count
             vt, sbt, dtt, _ = res[threads]
             impl_desc = ("util/crc32c.cc of the reference (portable path, g++ -O3, oracle/_ref), each thread pinned "
