@@ -1071,13 +1071,15 @@ def batch_results(mem: Memory, f: dict, published: bool = True):
 
 def run_batch_kernel(asm: str, name: str, threads: int, data: np.ndarray, off, ln, tabs: bytes, wg: int = 0,
                      grid: int = 256, hint: int = 0, expect=None, lds_bytes: int = 160768, last: bool = True,
-                     state: dict | None = None):
+                     state: dict | None = None, init=None):
     """Run workgroup `wg` of a batch kernel (a PiecesArgs kernel in static, unplanned mode) over the given batch.
     Verify form: with `last` the other grid - 1 workgroups count as arrived, so this one publishes the verdict; without
     it, it is an early one and `state` (a dict) receives the accumulators it leaves.
     Returns (out words, mask of blocks written, first_bad or -1, nbad, instructions executed)."""
     mem, f = batch_memory(data, off, ln, tabs, expect, last_of=(wg, grid) if last else None)
     f["hint"] = hint
+    if init is not None:  # per-block initial CRCs (Extend(init[i], block i))
+        f["init"] = mem.alloc(4 * len(init), data=np.asarray(init, np.uint32))
     steps = launch(mem, asm, name, threads, lds_bytes, f, grid, [wg])
     if state is not None and "vacc" in f:
         state["vacc"] = accumulators(mem, f)

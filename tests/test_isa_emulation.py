@@ -130,6 +130,11 @@ def test_emulated_wide_unplanned(env, verify):
                                                lds_bytes=160768)
     mine = np.nonzero(written)[0]
     assert mine.size > 0 and np.array_equal(out[mine], exp[mine])
+    # per-block initial CRCs: the padded head rewinds each block's register to its 16-B boundary (x^-8k)
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    exp_i = load_oracle().batch(data, off, ln, init, threads=8)
+    out_i, wi, _, _, _ = E.run_batch_kernel(ASM, PIECES % (0, 0, 0), 512, data, off, ln, tabs, wg=7, init=init)
+    assert np.array_equal(np.nonzero(wi)[0], mine) and np.array_equal(out_i[mine], exp_i[mine])
     if verify:
         plant = mine[[0, mine.size - 1]]
         out_v, wv, fb, nb, _ = E.run_batch_kernel(ASM, PIECES % (0, 0, 1), 512, data, off, ln, tabs, wg=7,
