@@ -1389,7 +1389,9 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_claim_kernel(PiecesArg
       if (!step(nxt, T, cur, S)) break;
     }
   }
-  if (kVerify) verify_publish(a, wave);
+  // two-level arrival: the claims balance the run, so the 256 workgroups end within a µs of each other (bunched, as
+  // the combine kernel's do), unlike the other narrow forms' staircase of workgroup ends
+  if (kVerify) verify_publish<kVaccShards>(a, wave);
 }
 
 // Bitonic sort of one (key, idx) pair per lane over the wavefront, ascending by key (ties by idx, so the two

@@ -1027,11 +1027,12 @@ def launch(mem: Memory, asm: str, name: str, threads: int, lds_bytes: int, field
 SENTINEL = 0xDEADBEEF
 
 
-def batch_memory(data, off, ln, tabs: bytes, expect=None, last_of=None):
+def batch_memory(data, off, ln, tabs: bytes, expect=None, last_of=None, shards: int = 1):
     """Device image of one batch call: payload, descriptors, results (sentinel-filled), tables, verify words.  The
     caller's result words start as a sentinel (the kernels must write them); the accumulators in their reset state,
-    except with last_of = (wg, grid): every other workgroup of the grid counts as arrived already (its shard's and the
-    other shards'), so emulating that one workgroup is the last, publishing one."""
+    except with last_of = (wg, grid): every other workgroup of the grid counts as arrived already, so emulating that
+    one workgroup is the last, publishing one (shards > 1: a two-level arrival, verify_publish<kShards>: the rest of
+    its shard on the shard word, the other shards' last workgroups on the final word)."""
     n = int(np.asarray(off).size)
     mem = Memory()
     f = {"base": mem.alloc(data.size + 65536, data=data), "off": mem.alloc(8 * n, data=np.asarray(off, np.uint64)),
@@ -1044,9 +1045,14 @@ def batch_memory(data, off, ln, tabs: bytes, expect=None, last_of=None):
         f["nbad"] = mem.alloc(8, data=np.array([SENTINEL], np.uint64))
         v = np.zeros(VACC_STRIDE * (1 + VACC_SHARDS), np.uint64)
         v[0] = ~np.uint64(0)
-        if last_of is not None:  # the CRC kernels arrive on the final word directly (one level)
+        if last_of is not None:
             wg, grid = last_of
-            v[1] = np.uint64(grid - 1) << np.uint64(40)
+            if shards == 1:  # one level: every workgroup on the final word
+                v[1] = np.uint64(grid - 1) << np.uint64(40)
+            else:
+                sh = wg % shards
+                v[VACC_STRIDE * (1 + sh)] = np.uint64((grid - sh + shards - 1) // shards - 1) << np.uint64(40)
+                v[1] = np.uint64(min(grid, shards) - 1) << np.uint64(40)
         f["vacc"] = mem.alloc(8 * v.size, data=v)
     return mem, f
 
@@ -1071,12 +1077,12 @@ def batch_results(mem: Memory, f: dict, published: bool = True):
 
 def run_batch_kernel(asm: str, name: str, threads: int, data: np.ndarray, off, ln, tabs: bytes, wg: int = 0,
                      grid: int = 256, hint: int = 0, expect=None, lds_bytes: int = 160768, last: bool = True,
-                     state: dict | None = None, init=None):
+                     state: dict | None = None, init=None, shards: int = 1):
     """Run workgroup `wg` of a batch kernel (a PiecesArgs kernel in static, unplanned mode) over the given batch.
     Verify form: with `last` the other grid - 1 workgroups count as arrived, so this one publishes the verdict; without
     it, it is an early one and `state` (a dict) receives the accumulators it leaves.
     Returns (out words, mask of blocks written, first_bad or -1, nbad, instructions executed)."""
-    mem, f = batch_memory(data, off, ln, tabs, expect, last_of=(wg, grid) if last else None)
+    mem, f = batch_memory(data, off, ln, tabs, expect, last_of=(wg, grid) if last else None, shards=shards)
     f["hint"] = hint
     if init is not None:  # per-block initial CRCs (Extend(init[i], block i))
         f["init"] = mem.alloc(4 * len(init), data=np.asarray(init, np.uint32))

@@ -32,7 +32,9 @@ SORTED = "_ZN5kvsep27crc32c_narrow_sorted_kernelILi4ELb1ELi1024ELb0ELi0ELb%dEEEv
 NARROW16 = "_ZN5kvsep20crc32c_narrow_kernelILi4ELb1ELi1024ELb0ELi0ELb1ENS_7LdsFullELb%dEEEvNS_10PiecesArgsE"
 NARROW8 = "_ZN5kvsep20crc32c_narrow_kernelILi4ELb1ELi512ELb1ELi0ELb1ENS_7LdsFullELb%dEEEvNS_10PiecesArgsE"
 CLAIM = "_ZN5kvsep26crc32c_narrow_claim_kernelILi4ELi512ELb%dEEEvNS_10PiecesArgsE"
-KERNELS = [("sorted", SORTED, 1024), ("narrow16", NARROW16, 1024), ("narrow8", NARROW8, 512), ("claim", CLAIM, 512)]
+# (label, template, threads per workgroup, arrival levels of the verify publish: 8 = per-XCD shards, then the final word)
+KERNELS = [("sorted", SORTED, 1024, 1), ("narrow16", NARROW16, 1024, 1), ("narrow8", NARROW8, 512, 1),
+           ("claim", CLAIM, 512, 8)]
 
 
 @pytest.fixture(scope="module")
@@ -62,8 +64,8 @@ def batch(kind, splitmix64_bytes):
 
 
 @pytest.mark.parametrize("kind", ["short", "long"])
-@pytest.mark.parametrize("label,tmpl,threads", KERNELS)
-def test_emulated_kernel_matches_oracle(env, label, tmpl, threads, kind):
+@pytest.mark.parametrize("label,tmpl,threads,shards", KERNELS)
+def test_emulated_kernel_matches_oracle(env, label, tmpl, threads, shards, kind):
     E, tabs, mask, splitmix64_bytes = env
     data, off, ln, hint = batch(kind, splitmix64_bytes)
     exp = load_oracle().batch(data, off, ln, None, threads=8)
@@ -79,29 +81,33 @@ def test_emulated_kernel_matches_oracle(env, label, tmpl, threads, kind):
     plant = mine[[0, mine.size // 2, mine.size - 1]]
     stored[plant] ^= 0x100
     out_v, written_v, fb, nb, _ = E.run_batch_kernel(ASM, tmpl % 1, threads, data, off, ln, tabs, wg=wg, hint=hint,
-                                                    expect=stored)
+                                                    expect=stored, shards=shards)
     assert np.array_equal(np.nonzero(written_v)[0], mine)
     assert np.array_equal(out_v[mine], exp[mine])
     assert (fb, nb) == (int(plant.min()), 3)  # published by this (last) workgroup, accumulators reset (batch_results)
-    _verify_tail(E, tmpl % 1, threads, data, off, ln, tabs, wg, hint, exp, mask, mine, plant)
+    _verify_tail(E, tmpl % 1, threads, data, off, ln, tabs, wg, hint, exp, mask, mine, plant, shards=shards)
 
 
-def _verify_tail(E, name, threads, data, off, ln, tabs, wg, hint, exp, mask, mine, plant, lds_bytes=160768):
+def _verify_tail(E, name, threads, data, off, ln, tabs, wg, hint, exp, mask, mine, plant, lds_bytes=160768, shards=1):
     """The verify form's end (verify_publish): a clean batch publishes (-1, 0) from the last workgroup; a workgroup that
     is not the last leaves the caller's words alone and its posts -- lowest index, count, one arrival -- in the
     accumulators for the last one."""
     clean = np.array([mask(int(x)) for x in exp], np.uint32)
     *_, fb, nb, _ = E.run_batch_kernel(ASM, name, threads, data, off, ln, tabs, wg=wg, hint=hint, expect=clean,
-                                       lds_bytes=lds_bytes)
+                                       lds_bytes=lds_bytes, shards=shards)
     assert (fb, nb) == (-1, 0)
     stored = clean.copy()
     stored[plant] ^= 0x100
     st = {}
     *_, fb, nb, _ = E.run_batch_kernel(ASM, name, threads, data, off, ln, tabs, wg=wg, hint=hint, expect=stored,
-                                       lds_bytes=lds_bytes, last=False, state=st)
+                                       lds_bytes=lds_bytes, last=False, state=st, shards=shards)
     assert (fb, nb) == (E.SENTINEL, E.SENTINEL)  # not published
-    # one arrival and the count on the final word; the shard words belong to the combine kernel's two-level arrival
-    assert st["vacc"] == (int(plant.min()), (1 << 40) | len(plant)) + (0,) * E.VACC_SHARDS, [hex(v) for v in st["vacc"]]
+    # the count on the final word; the arrival there (one level) or on the workgroup's shard word (two levels)
+    sh = [0] * E.VACC_SHARDS
+    if shards > 1:
+        sh[wg % shards] = 1 << 40
+    final = len(plant) | ((1 << 40) if shards == 1 else 0)
+    assert st["vacc"] == (int(plant.min()), final, *sh), [hex(v) for v in st["vacc"]]
 
 
 PIECES = "_ZN5kvsep20crc32c_pieces_kernelILb%dELb%dELi4ELb1ELb1ELi0ELi512ELb1ELb%dEEEvNS_10PiecesArgsE"
