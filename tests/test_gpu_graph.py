@@ -38,7 +38,7 @@ def test_capture_and_replay(layout, oracle):
     try:
         ctx.reserve(off.size, int(ln.sum()))
         assert ctx.kernel_name(off.size, int(ln.max())) == (
-            "crc32c_pieces_kernel" if layout == "planned" else "crc32c_narrow_claim_kernel")  # 20,000 x 4 KiB
+            "crc32c_pieces_kernel" if layout == "planned" else "crc32c_narrow_kernel")  # 20,000 x 4 KiB: 16 waves
         kvsep.fill_splitmix64(data.data_ptr(), span, 1, 0)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
