@@ -282,6 +282,13 @@ template <int kG, bool kNT, int kAbl = 0, bool kAlign = false, bool kPad = false
           typename Next>  // kAbl != 0: ablations (wrong)
 __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, uint32_t reg, uint32_t lane,
                                            uint32_t lc0, uint32_t lc1, Next&& next) {
+  if (kAbl == 7 && s.K <= uint64_t(kG)) {  // ablation: a short item's chain is free (its loads are still used)
+    next();
+    uint32_t x = reg ^ s.v.x ^ s.v.w ^ s.et.x ^ s.tc.y ^ s.hc.z;
+#pragma unroll
+    for (int i = 0; i < kG; ++i) x ^= s.A[i].x ^ s.A[i].y ^ s.A[i].z ^ s.A[i].w;
+    return x;
+  }
   if (s.K) {
     const uint64_t K = s.K, last = K - 1;
     if (kAbl != 3 && s.ps < s.h0) reg = serial16(lds, reg, uniform4(s.hc), int(s.ps - s.hbase), int(s.h0 - s.hbase));
