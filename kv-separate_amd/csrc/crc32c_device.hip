@@ -1285,7 +1285,10 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
 // with no claims measured within 1 % of the claims: most of the gain is the workgroup-contiguous run itself.  Blocks
 // over the hint go to narrow_deferred right after their group (8 waves have the VGPRs for it inline).
 // kVerify: the verify form (stored words loaded before each group's remaining rows, verify_wave, verify_publish).
-template <int kG, int kThreads, bool kVerify = false>
+// kOverlap (shipped): the first group's rows are staged between the fill's table loads and its LDS stores, so the
+// first HBM round trip runs under the fill (diag variant 59 = without: 4 KiB blocks 128 MiB 25.60 -> 24.84 us, 256 MiB
+// 44.75 -> 44.15, 512 MiB 81.83 -> 81.29, 1 GiB 156.09 -> 154.77; profiles/round4/claim_shapes/).
+template <int kG, int kThreads, bool kVerify = false, bool kOverlap = true>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_claim_kernel(PiecesArgs a) {
   constexpr uint32_t kWaves = kThreads / 64, kPerGroup = 64 / kNarrowLanes, kNone = 0xffffffffu;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -1383,12 +1386,17 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_claim_kernel(PiecesArg
   // the wave's first group is static (the wave's slot of the run), its descriptors fetched during the LDS fill
   uint32_t g0 = run0 + wave < run1 ? run0 + wave : kNone;
   load_desc(g0, dn);
-  fill_lds<kThreads, true>(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
-  __syncthreads();
+  CItem cur, nxt;
+  NStaged<kG> S, T;
+  if (kOverlap) {  // unconditional: a wave with no group stages an empty one (the stores' wait count is fixed)
+    fill_lds<kThreads, true>(lds, &a.tabs->znarrow[0][0], a.tabs, tid, [&]() { take(g0, cur, S); });
+    __syncthreads();
+  } else {
+    fill_lds<kThreads, true>(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
+    __syncthreads();
+  }
   if (g0 != kNone) {
-    CItem cur, nxt;
-    NStaged<kG> S, T;
-    take(g0, cur, S);
+    if (!kOverlap) take(g0, cur, S);
     gn = next_group();
     load_desc(gn, dn);
     for (;;) {
