@@ -1291,6 +1291,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
 template <int kG, int kThreads, bool kVerify = false, bool kOverlap = true>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_claim_kernel(PiecesArgs a) {
   constexpr uint32_t kWaves = kThreads / 64, kPerGroup = 64 / kNarrowLanes, kNone = 0xffffffffu;
+  [[maybe_unused]] constexpr uint32_t kWavesPerWg = kWaves;  // the stamp hooks' name for it
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   __shared__ uint32_t claimed;  // groups of the run claimed after each wave's first (static) one
   const uint32_t tid = threadIdx.x;
@@ -1384,6 +1385,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_claim_kernel(PiecesArg
   };
 
   // the wave's first group is static (the wave's slot of the run), its descriptors fetched during the LDS fill
+  KVSEP_NSTAMP_ENTRY();  // stamp hooks (crc32c_hooks.inc): empty in the shipped library
   uint32_t g0 = run0 + wave < run1 ? run0 + wave : kNone;
   load_desc(g0, dn);
   CItem cur, nxt;
@@ -1395,15 +1397,19 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_claim_kernel(PiecesArg
     fill_lds<kThreads, true>(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
     __syncthreads();
   }
+  KVSEP_NSTAMP(1);
   if (g0 != kNone) {
     if (!kOverlap) take(g0, cur, S);
     gn = next_group();
     load_desc(gn, dn);
-    for (;;) {
+    for (;;) {  // (stamps: after each group but a wave's last)
       if (!step(cur, S, nxt, T)) break;
+      KVSEP_NSTEP();
       if (!step(nxt, T, cur, S)) break;
+      KVSEP_NSTEP();
     }
   }
+  KVSEP_NSTAMP(7);
   // two-level arrival: the claims balance the run, so the 256 workgroups end within a µs of each other (bunched, as
   // the combine kernel's do), unlike the other narrow forms' staircase of workgroup ends
   if (kVerify) verify_publish<kVaccShards>(a, wave);

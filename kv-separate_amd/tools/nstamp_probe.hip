@@ -3,7 +3,7 @@
 // spread (p10 / p50 / p90 / max, us) of each stamp over all waves: where a small batch's time goes (launch ramp,
 // fill, first data, last-group compute tail).  Never used for timing numbers.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o nstamp_probe nstamp_probe.hip
-// Usage: nstamp_probe <block_len> <count> <kernel: 3 = narrow 16 waves, 4 = narrow 8 waves>
+// Usage: nstamp_probe <block_len> <count> <kernel: 3 = narrow 16 waves, 4 = narrow 8 waves, 6 = claim>
 #define KVSEP_STAMPS 1
 #include "../csrc/crc32c_device.hip"
 #include "../csrc/crc32c_host.cpp"
