@@ -682,9 +682,14 @@ __device__ __forceinline__ void fill_lds_compact(uint8_t* lds, const uint32_t* r
 // One workgroup per CU in every case (the LDS image is 157 KiB).
 // kVerify: the verify form -- each whole block this kernel emits is checked against a.expect (verify_uniform); the
 // pieces of split blocks are checked by the combine kernel, which produces their CRC.
+// kStrided (diag variants 27 / 28, static): a sweeping deal -- wave v takes items v, v + nwaves, v + 2 nwaves, ..., so
+// at any time the waves stream neighbouring pieces of one window that moves through the batch; its descriptor windows
+// hold the wave's next 64 items of that stride, resolved as in the contiguous modes.  v is numbered workgroup-major
+// (kStrided 1: a CU's waves on neighbouring pieces) or wave-major (2: neighbouring pieces on different CUs and XCDs).
 template <bool kPlanned, bool kDynamic, int kG, bool kNT, bool kAhead, int kAbl = 0, int kThreads = kWgThreads,
-          bool kAlign = true, bool kVerify = false>
+          bool kAlign = true, bool kVerify = false, int kStrided = 0>
 __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
+  static_assert(!(kStrided && kDynamic), "the sweeping deal is static");
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   // the padded head (stage<kPad>); diag variant 26 (kAbl == 6) keeps the serial head of rounds 1-3 for A/B: measured
   // 3a -0.8 / -1.8 %, config 4 -0.1 / -0.2 %, 3b and config 4's short blocks equal, in one process on two boxes
@@ -730,8 +735,13 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
     gdiv = total / (64 * nwaves);
     gdiv = gdiv < 4 ? 4 : gdiv > 32 ? 32 : gdiv;
   }
+  const uint64_t istep = kStrided ? nwaves : 1;  // item stride inside a descriptor window
   auto grab = [&]() -> bool {
-    if (kDynamic) {
+    if (kStrided) {
+      if (lo != ~uint64_t(0)) return false;
+      lo = kStrided == 1 ? uint64_t(blockIdx.x) * kWavesPerWg + wave : uint64_t(wave) * gridDim.x + blockIdx.x;
+      hi = total;
+    } else if (kDynamic) {
       const uint64_t rem = total > seen ? total - seen : 0;
       uint64_t c = rem / (gdiv * nwaves);
       if (a.guided_cap && c > a.guided_cap) c = a.guided_cap;
@@ -762,10 +772,10 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   uint32_t w_b = 0, w_reg0 = 0, w_only = 0, w_exp = 0;
   auto fill_set = [&](uint64_t start, uint64_t n, uintptr_t& w_ps, uintptr_t& w_pe, uint32_t& w_b, uint32_t& w_reg0,
                       uint32_t& w_only, uint32_t& w_exp) {
-    const uint64_t g = start + lane;
+    const uint64_t g = start + lane * istep;
     w_ps = w_pe = 0;
     w_b = w_reg0 = w_only = w_exp = 0;
-    if (g < start + n) {
+    if (kStrided ? lane < n : g < start + n) {
       uint64_t b, rs, re;
       bool first, only;
       if (planned) {
@@ -796,7 +806,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   };
   auto fill = [&](uint64_t start, uint64_t stop) {
     w0 = start;
-    wn = stop - start < 64 ? stop - start : 64;
+    const uint64_t left = kStrided ? (stop - start + istep - 1) / istep : stop - start;
+    wn = left < 64 ? left : 64;
     fill_set(w0, wn, w_ps, w_pe, w_b, w_reg0, w_only, w_exp);
   };
   struct Item {
@@ -805,7 +816,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
     bool only;
   };
   auto take = [&](uint64_t g, Item& it, Staged<kG>& st) {  // item g of the window -> stage its loads
-    const uint32_t i = uint32_t(g - w0);
+    const uint32_t i = kStrided ? uint32_t(g - w0) / uint32_t(istep) : uint32_t(g - w0);
     // readlane returns int: go through uint32_t so nothing is sign-extended into the upper half
     auto rl = [i](uint32_t v) -> uint32_t { return uint32_t(__builtin_amdgcn_readlane(int(v), int(i))); };
     it.g = g;
@@ -831,16 +842,16 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   // roles of the two buffers (ping-pong) instead of copying B into A after each item: such a copy must wait
   // for ALL of B's loads (vmcnt(0)) and would put a full HBM latency back on every item.
   auto step = [&](uint64_t g, uint64_t end, Item& ia, Staged<kG>& A, Item& ib, Staged<kG>& B) {
-    const bool hn = g + 1 < end;
+    const bool hn = g + istep < end;
     KVSEP_WSTAMP_ITEM_BEGIN();
     // The next item's HBM loads overlap the end of this item's compute (finish() stages them late, see
     // there).  The take is unconditional (the last item re-stages itself): on a path without it, this item's loads would be the most recent ones and the
     // compiler's counted wait (which merges both paths) would drain everything, vmcnt(0), on every item.
     emit(ia, finish<kG, kNT, kAbl, kAlign, kPad>(lds, A, ia.reg0, lane, lc0, lc1, [&]() {
-           if (kAhead) take(hn ? g + 1 : g, ib, B);
+           if (kAhead) take(hn ? g + istep : g, ib, B);
          }));
     KVSEP_WSTAMP_ITEM_END(ia);
-    if (!kAhead && hn) take(g + 1, ib, B);
+    if (!kAhead && hn) take(g + istep, ib, B);
     return hn;
   };
 
@@ -850,13 +861,13 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   __syncthreads();
   KVSEP_WSTAMP_FILLED();
   while (grab()) {
-    for (uint64_t ws = lo; ws < hi; ws += 64) {
+    for (uint64_t ws = lo; ws < hi; ws += 64 * istep) {
       fill(ws, hi);
-      const uint64_t end = w0 + wn;
+      const uint64_t end = w0 + wn * istep;
       take(w0, cur, S);
-      for (uint64_t g = w0;; g += 2) {
+      for (uint64_t g = w0;; g += 2 * istep) {
         if (!step(g, end, cur, S, nxt, T)) break;
-        if (!step(g + 1, end, nxt, T, cur, S)) break;
+        if (!step(g + istep, end, nxt, T, cur, S)) break;
       }
     }
   }
