@@ -908,10 +908,11 @@ struct NStaged {
 struct NGeo {
   uint32_t P, E, h0, a1, ar;
 };
-template <bool kAlign>
+template <bool kAlign, int kL = kNarrowLanes>
 __device__ __forceinline__ NGeo ngeo(uintptr_t ps, uint32_t len) {
+  constexpr uint32_t kRow = 16u * kL;
   NGeo g;
-  g.P = uint32_t(ps) & (kNarrowRow - 1);
+  g.P = uint32_t(ps) & (kRow - 1);
   g.E = g.P + len;
   g.h0 = (g.P + 15u) & ~15u;
   if (g.h0 > g.E) g.h0 = g.E;
@@ -919,27 +920,27 @@ __device__ __forceinline__ NGeo ngeo(uintptr_t ps, uint32_t len) {
   if (g.a1 < g.h0) g.a1 = g.h0;
   g.ar = g.a1;
   if (kAlign) {
-    g.ar = g.a1 & ~(kNarrowRow - 1);
+    g.ar = g.a1 & ~(kRow - 1);
     if (g.ar < g.h0) g.ar = g.h0;
   }
   return g;
 }
 
-template <int kG, bool kNT, bool kAlign = true>
+template <int kG, bool kNT, bool kAlign = true, int kL = kNarrowLanes>
 __device__ __forceinline__ void nstage(NStaged<kG>& s, uintptr_t ps, uint32_t len, uint32_t j, uintptr_t dummy) {
+  constexpr uint32_t kRow = 16u * kL;
   s.ps = ps;
   s.len = len;
-  const NGeo g = ngeo<kAlign>(ps, len);
+  const NGeo g = ngeo<kAlign, kL>(ps, len);
   const uintptr_t line = ps - g.P;
-  s.K = (g.ar - g.h0 + kNarrowRow - 1) / kNarrowRow;
-  const int32_t rel0 = int32_t(g.ar - s.K * kNarrowRow + j * 16u);  // row 0's chunk, may start before the line
+  s.K = (g.ar - g.h0 + kRow - 1) / kRow;
+  const int32_t rel0 = int32_t(g.ar - s.K * kRow + j * 16u);  // row 0's chunk, may start before the line
   s.seg = line + intptr_t(rel0);
   const bool v_ok = s.K && rel0 >= int32_t(g.h0);
   s.hc = ld16(g.P < g.h0 ? line + (g.P & ~15u) : dummy);
   if (kAlign) {
     const uint32_t m = (g.a1 - g.ar) >> 4;
-    s.tc = ld16((j == kNarrowLanes - 1 ? g.a1 < g.E : j + m >= kNarrowLanes - 1) ? line + (g.a1 - 112u + j * 16u)
-                                                                                 : dummy);
+    s.tc = ld16((j == kL - 1 ? g.a1 < g.E : j + m >= kL - 1) ? line + (g.a1 - (kRow - 16u) + j * 16u) : dummy);
   } else {
     s.tc = ld16(g.a1 < g.E ? line + g.a1 : dummy);
   }
@@ -947,16 +948,20 @@ __device__ __forceinline__ void nstage(NStaged<kG>& s, uintptr_t ps, uint32_t le
   const uint32_t last = s.K > 1 ? s.K - 1 : 0;
 #pragma unroll
   for (int i = 0; i < kG; ++i)
-    s.A[i] = ld16<kNT>(last ? s.seg + uintptr_t(1 + i < int(last) ? 1 + i : last) * kNarrowRow : dummy);
+    s.A[i] = ld16<kNT>(last ? s.seg + uintptr_t(1 + i < int(last) ? 1 + i : last) * kRow : dummy);
 }
 
 // Raw register after the slot item, valid in the slot's last lane (j == 7).  kmin / kmax: wave min / max of K.
 // `next()` stages the following group, after this group's last row loads (see the wide kernel's finish()).
-template <int kG, bool kNT, int kAbl = 0, bool kAlign = true, typename Lay = LdsFull, typename Next>  // kAbl != 0: ablation (wrong)
+// kL: lanes per slot, 8 (Z_128 rows, a 3-level slot tree) or 16 (diag: Z_256 rows, 4 levels; LdsFull only).
+template <int kG, bool kNT, int kAbl = 0, bool kAlign = true, typename Lay = LdsFull, int kL = kNarrowLanes,
+          typename Next>  // kAbl != 0: ablation (wrong)
 __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, uint32_t reg, uint32_t j,
                                             uint32_t lc0, uint32_t lc1, uint32_t kmin, uint32_t kmax,
                                             uintptr_t dummy, Next&& next) {
-  const NGeo g = ngeo<kAlign>(s.ps, s.len);
+  static_assert(kL == 8 || (kL == 16 && !Lay::kCompact), "slots of 8 lanes, or 16 on the full LDS image");
+  constexpr uint32_t kRow = 16u * kL;
+  const NGeo g = ngeo<kAlign, kL>(s.ps, s.len);
   // what the end needs, packed in one 32-bit value computed here, live across the row loop (at 16 waves the kernel
   // sits at 128 VGPRs): bits 0-3 the bytes after a1, bits 4-6 (kAlign) m, the whole chunks [ar, a1)
   const uint32_t endg = (g.E - g.a1) | (g.a1 - g.ar);
@@ -983,7 +988,7 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
     for (; r + 2 * kG <= kmin; r += kG) {  // every slot has rows r .. r+2kG-1: no guards, no clamps
       uint4 B[kG];
 #pragma unroll
-      for (int i = 0; i < kG; ++i) B[i] = ld16<kNT>(s.seg + uintptr_t(r + kG + i) * kNarrowRow);
+      for (int i = 0; i < kG; ++i) B[i] = ld16<kNT>(s.seg + uintptr_t(r + kG + i) * kRow);
       __builtin_amdgcn_sched_barrier(0);  // loads go out before the group's compute
 #pragma unroll
       for (int i = 0; i < kG; ++i) KVSEP_NROW(s.A[i]);
@@ -995,7 +1000,7 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
       const uint32_t nr = r + kG;
 #pragma unroll
       for (int i = 0; i < kG; ++i)
-        B[i] = ld16<kNT>(last ? s.seg + uintptr_t(nr + i < last ? nr + i : last) * kNarrowRow : dummy);
+        B[i] = ld16<kNT>(last ? s.seg + uintptr_t(nr + i < last ? nr + i : last) * kRow : dummy);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < kG; ++i)
@@ -1024,6 +1029,10 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
       const uint32_t o = row_shr<4>(p);
       if ((j & 7u) == 7u) p = zmap_x(lds, Lay::kTree + 8192u, o, p);
     }
+    if (kL == 16) {  // a 16-lane slot is one DPP row: the 4th level (Z_128)
+      const uint32_t o = row_shr<8>(p);
+      if ((j & 15u) == 15u) p = zmap_x(lds, Lay::kTree + 12288u, o, p);
+    }
     if (K) reg = zmap(lds, Lay::kZ4, p);  // lane 7 of the slot: pending word at the rows' end - 4 -> register there
   }
   if (kAlign) {
@@ -1031,7 +1040,7 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
     if (__builtin_amdgcn_ballot_w64(m != 0)) {  // whole chunks [ar, a1) in lanes 7-m .. 6 of the tail load
       // their raw register from 0: per lane the STEP4W re-injection, moved up one lane (chunks in lanes 8-m .. 7),
       // the slot's 3-level tree; then R = Z_16m(register at ar) ^ that (Z_16m from the tree tables by the bits of m)
-      const uint4 e = j < kNarrowLanes - 1 && j + m >= kNarrowLanes - 1 ? s.tc : make_uint4(0, 0, 0, 0);
+      const uint4 e = j < kL - 1 && j + m >= kL - 1 ? s.tc : make_uint4(0, 0, 0, 0);
       uint32_t p = zmap_x(lds, Lay::kZ4, e.x, e.y);
       p = zmap_x(lds, Lay::kZ4, p, e.z);
       p = zmap_x(lds, Lay::kZ4, p, e.w);
@@ -1048,9 +1057,14 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
         const uint32_t o = row_shr<4>(p);
         if ((j & 7u) == 7u) p = zmap_x(lds, Lay::kTree + 8192u, o, p);
       }
+      if (kL == 16) {
+        const uint32_t o = row_shr<8>(p);
+        if ((j & 15u) == 15u) p = zmap_x(lds, Lay::kTree + 12288u, o, p);
+      }
       if (m & 1u) reg = zmap(lds, Lay::kTree, reg);
       if (m & 2u) reg = zmap(lds, Lay::kTree + 4096u, reg);
       if (m & 4u) reg = zmap(lds, Lay::kTree + 8192u, reg);
+      if (kL == 16 && (m & 8u)) reg = zmap(lds, Lay::kTree + 12288u, reg);
       reg ^= zmap(lds, Lay::kZ4, p);  // lane 7: register at a1
     }
   }
@@ -1062,17 +1076,17 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
 // [lo, hi) again and checksums those blocks one at a time, each cut into parts of <= 1 GiB, 8 at a time (one per
 // slot; the slot geometry is 32-bit), merged with R(A||B) = Z_|B|(R(A)) ^ R(B) through gf2_shift.  Slower than the
 // main path (long blocks are not what the narrow kernels are for) but exact for any 64-bit length.
-template <int kG, bool kNT, bool kAlignN, typename Lay = LdsFull, bool kVerify = false>
+template <int kG, bool kNT, bool kAlignN, typename Lay = LdsFull, bool kVerify = false, int kL = kNarrowLanes>
 __device__ __forceinline__ void narrow_deferred(const PiecesArgs& a, const uint8_t* lds, uint64_t lo, uint64_t hi,
                                                 uintptr_t dummy) {
-  constexpr uint32_t kPerGroup = 64 / kNarrowLanes;
+  constexpr uint32_t kPerGroup = 64 / kL;
   // The lane constants are recomputed here (volatile, so not merged with the kernel's own): values kept live across
   // the main group loop for this rarely taken walk would cost registers at the 16-wave kernels' 128-VGPR cap.
   uint32_t lane;
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
   const uint32_t lc0 = Lay::lc0(lane), lc1 = Lay::lc1(lane);
-  const uint32_t j = lane & (kNarrowLanes - 1);
-  const uint32_t slot = lane / kNarrowLanes;
+  const uint32_t j = lane & (kL - 1);
+  const uint32_t slot = lane / kL;
   const uint32_t hint32 = uint32_t(a.hint);
   struct Desc {
     uint64_t off;
@@ -1093,9 +1107,9 @@ __device__ __forceinline__ void narrow_deferred(const PiecesArgs& a, const uint8
       load_desc(g, d);
       uint64_t over = __builtin_amdgcn_ballot_w64(g + slot < hi && (d.lenhi != 0 || d.len > hint32));
       while (over) {
-        const uint32_t k = uint32_t(__builtin_ctzll(over)) / kNarrowLanes;  // slot of the next deferred block
-        over &= ~(0xffull << (k * kNarrowLanes));
-        const uint32_t src = k * kNarrowLanes;
+        const uint32_t k = uint32_t(__builtin_ctzll(over)) / kL;  // slot of the next deferred block
+        over &= ~(((1ull << kL) - 1) << (k * kL));
+        const uint32_t src = k * kL;
         const uint64_t boff = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(d.off >> 32)), int(src)))) << 32) |
                               uint32_t(__builtin_amdgcn_readlane(int(uint32_t(d.off)), int(src)));
         const uint64_t L = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(d.lenhi), int(src)))) << 32) |
@@ -1113,20 +1127,20 @@ __device__ __forceinline__ void narrow_deferred(const PiecesArgs& a, const uint8
           const uint64_t rs = p < nparts ? p * q : L;
           const uint64_t re = rs + q < L ? rs + q : L;
           NStaged<kG> X;
-          nstage<kG, kNT, kAlignN>(X, blk + rs, uint32_t(re - rs), j, dummy);
+          nstage<kG, kNT, kAlignN, kL>(X, blk + rs, uint32_t(re - rs), j, dummy);
           uint32_t km = 0, kn = ~0u;
 #pragma unroll
           for (uint32_t t = 0; t < kPerGroup; ++t) {
-            const uint32_t kk = uint32_t(__builtin_amdgcn_readlane(int(X.K), int(t * kNarrowLanes)));
+            const uint32_t kk = uint32_t(__builtin_amdgcn_readlane(int(X.K), int(t * kL)));
             km = km > kk ? km : kk;
             kn = kn < kk ? kn : kk;
           }
-          uint32_t reg = nfinish<kG, kNT, 0, kAlignN, Lay>(lds, X, p == 0 ? ~binit : 0u, j, lc0, lc1, kn, km, dummy,
+          uint32_t reg = nfinish<kG, kNT, 0, kAlignN, Lay, kL>(lds, X, p == 0 ? ~binit : 0u, j, lc0, lc1, kn, km, dummy,
                                                          NoMid());
-          if (j == kNarrowLanes - 1) reg = gf2_shift(a.tabs, reg, L - re);  // carried to the block's end
+          if (j == kL - 1) reg = gf2_shift(a.tabs, reg, L - re);  // carried to the block's end
 #pragma unroll
           for (uint32_t t = 0; t < kPerGroup; ++t)
-            acc ^= uint32_t(__builtin_amdgcn_readlane(int(reg), int(t * kNarrowLanes + kNarrowLanes - 1)));
+            acc ^= uint32_t(__builtin_amdgcn_readlane(int(reg), int(t * kL + kL - 1)));
         }
         if (lane == 0) emit_block(a, g + k, ~acc);
         // acc is wave-uniform (a readlane sum); so is the stored word, read through readfirstlane
@@ -1299,16 +1313,17 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
 // kOverlap (shipped): the first group's rows are staged between the fill's table loads and its LDS stores, so the
 // first HBM round trip runs under the fill (diag variant 59 = without: 4 KiB blocks 128 MiB 25.60 -> 24.84 us, 256 MiB
 // 44.75 -> 44.15, 512 MiB 81.83 -> 81.29, 1 GiB 156.09 -> 154.77; profiles/round4/claim_shapes/).
-template <int kG, int kThreads, bool kVerify = false, bool kOverlap = true>
+// kL (diag variant 60): lanes per slot -- 16 makes a group 4 blocks (Z_256 rows, the tree tables' Z_256 replicated).
+template <int kG, int kThreads, bool kVerify = false, bool kOverlap = true, int kL = kNarrowLanes>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_claim_kernel(PiecesArgs a) {
-  constexpr uint32_t kWaves = kThreads / 64, kPerGroup = 64 / kNarrowLanes, kNone = 0xffffffffu;
+  constexpr uint32_t kWaves = kThreads / 64, kPerGroup = 64 / kL, kNone = 0xffffffffu;
   [[maybe_unused]] constexpr uint32_t kWavesPerWg = kWaves;  // the stamp hooks' name for it
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   __shared__ uint32_t claimed;  // groups of the run claimed after each wave's first (static) one
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
-  const uint32_t j = lane & (kNarrowLanes - 1);
-  const uint32_t slot = lane / kNarrowLanes;
+  const uint32_t j = lane & (kL - 1);
+  const uint32_t slot = lane / kL;
   const uint32_t lc0 = LdsFull::lc0(lane), lc1 = LdsFull::lc1(lane);
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uintptr_t dummy = reinterpret_cast<uintptr_t>(a.tabs);
@@ -1361,12 +1376,12 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_claim_kernel(PiecesArg
     it.g = g;
     it.over = over;
     it.reg0 = ~dn.init;
-    nstage<kG, true, true>(st, live ? reinterpret_cast<uintptr_t>(a.base) + dn.off : dummy, live ? dn.len : 0u, j,
+    nstage<kG, true, true, kL>(st, live ? reinterpret_cast<uintptr_t>(a.base) + dn.off : dummy, live ? dn.len : 0u, j,
                            dummy);
     uint32_t km = 0, kn = ~0u;
 #pragma unroll
     for (uint32_t k = 0; k < kPerGroup; ++k) {
-      const uint32_t kk = uint32_t(__builtin_amdgcn_readlane(int(st.K), int(k * kNarrowLanes)));
+      const uint32_t kk = uint32_t(__builtin_amdgcn_readlane(int(st.K), int(k * kL)));
       km = km > kk ? km : kk;
       kn = kn < kk ? kn : kk;
     }
@@ -1382,13 +1397,13 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_claim_kernel(PiecesArg
       ex = ld32(a.expect + g0 + (slot < last ? slot : uint32_t(last)));
       __builtin_amdgcn_sched_barrier(0);
     }
-    const uint32_t reg = nfinish<kG, true, 0, true>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
+    const uint32_t reg = nfinish<kG, true, 0, true, LdsFull, kL>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
                                                     [&]() { take(gn, ib, B); });
-    const bool mine = j == kNarrowLanes - 1 && g0 + slot < count && !ia.over;
+    const bool mine = j == kL - 1 && g0 + slot < count && !ia.over;
     if (kVerify) verify_wave(a, lane, mine, g0, slot, ~reg, ex);  // before the store
     if (mine) emit_block(a, g0 + slot, ~reg);
     if (ia.deferred)  // wave-uniform: this group's blocks over the hint, whole
-      narrow_deferred<kG, true, true, LdsFull, kVerify>(a, lds, g0, g0 + kPerGroup < count ? g0 + kPerGroup : count,
+      narrow_deferred<kG, true, true, LdsFull, kVerify, kL>(a, lds, g0, g0 + kPerGroup < count ? g0 + kPerGroup : count,
                                                         dummy);
     gn = next_group();  // the group after ib: claimed now, its descriptors loaded while ib runs
     load_desc(gn, dn);
@@ -1401,11 +1416,12 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_claim_kernel(PiecesArg
   load_desc(g0, dn);
   CItem cur, nxt;
   NStaged<kG> S, T;
+  const uint32_t* rep = kL == 8 ? &a.tabs->znarrow[0][0] : &a.tabs->ztree[4][0][0];  // Z_{16 kL}
   if (kOverlap) {  // unconditional: a wave with no group stages an empty one (the stores' wait count is fixed)
-    fill_lds<kThreads, true>(lds, &a.tabs->znarrow[0][0], a.tabs, tid, [&]() { take(g0, cur, S); });
+    fill_lds<kThreads, kL == 8>(lds, rep, a.tabs, tid, [&]() { take(g0, cur, S); });
     __syncthreads();
   } else {
-    fill_lds<kThreads, true>(lds, &a.tabs->znarrow[0][0], a.tabs, tid);
+    fill_lds<kThreads, kL == 8>(lds, rep, a.tabs, tid);
     __syncthreads();
   }
   KVSEP_NSTAMP(1);
