@@ -80,7 +80,8 @@ int kvsep_crc32c_ctx_set_schedule(kvsep_crc32c_ctx* ctx, int dynamic);
  * form when the batch is ragged: max_len > 1.25 x total_bytes / count), 1 = always the wide kernel, 2 = the narrow
  * kernel whenever max_len <= 64 KiB, 3 / 4 = as 2 with 16- / 8-wave workgroups, 5 = as 2 in the sorted-window form,
  * 6 = as 2 with each workgroup's contiguous run of groups dealt to its waves by an LDS claim counter (round 4; auto
- * takes it for uniform batches of 32 Ki - 384 Ki blocks <= 4 KiB, 32 Ki - 64 Ki blocks <= 8 KiB).
+ * takes it for uniform batches of 32 Ki - 384 Ki blocks <= 4 KiB, 32 Ki - 64 Ki blocks of 4-8 KiB), 7 = as 6 with
+ * 16 lanes per block, 4-block groups (auto: uniform batches of >= 4 Ki blocks of 8-12 KiB, up to 512 MiB).
  * A choice of speed only: every kernel is exact for every block.  No environment variable changes it. */
 int kvsep_crc32c_ctx_set_kernel(kvsep_crc32c_ctx* ctx, int kernel);
 /* Pre-size scratch so later calls of up to `count` blocks / `total_bytes` bytes do not allocate

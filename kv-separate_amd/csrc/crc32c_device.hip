@@ -1313,7 +1313,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
 // kOverlap (shipped): the first group's rows are staged between the fill's table loads and its LDS stores, so the
 // first HBM round trip runs under the fill (diag variant 59 = without: 4 KiB blocks 128 MiB 25.60 -> 24.84 us, 256 MiB
 // 44.75 -> 44.15, 512 MiB 81.83 -> 81.29, 1 GiB 156.09 -> 154.77; profiles/round4/claim_shapes/).
-// kL (diag variant 60): lanes per slot -- 16 makes a group 4 blocks (Z_256 rows, the tree tables' Z_256 replicated).
+// kL: lanes per slot -- 16 makes a group 4 blocks (Z_256 rows, the tree tables' Z_256 replicated; narrow form 11, see
+// claim16_route; diag variant 60 is the same kernel).
 template <int kG, int kThreads, bool kVerify = false, bool kOverlap = true, int kL = kNarrowLanes>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_claim_kernel(PiecesArgs a) {
   constexpr uint32_t kWaves = kThreads / 64, kPerGroup = 64 / kL, kNone = 0xffffffffu;
@@ -1930,14 +1931,29 @@ bool ragged_batch(uint64_t count, uint64_t total_bytes, uint64_t max_len) {
   return count != 0 && total_bytes != 0 && 4 * max_len > 5 * (total_bytes / count);
 }
 
+// The claim kernel with 16-lane slots (form 11: 4-block groups of Z_256 rows) for uniform blocks of 8-12 KiB, from 4 Ki
+// of them up to 512 MiB.  Its groups are half the bytes of the 8-lane form's, so the waves' last groups end closer
+// together.  Measured against the routing before it in one process (profiles/round4/claim_shapes/claim16*.log, graph
+// replay, two boxes): 8 KiB blocks 32 MiB 11.05 vs 11.70 us, 64 MiB 15.73 vs 16.81, 128 MiB 23.94 / 24.14 vs 25.49 /
+// 25.29, 256 MiB 41.73 / 42.08 vs 43.78 / 44.08, 512 MiB 80.43 / 80.45 vs 81.73 / 82.07 (1 GiB equal); 10 KiB 64 MiB
+// 14.15 vs 19.89, 128 MiB 24.85 vs 31.30, 256 MiB 44.76 vs 44.13, 512 MiB 80.48 vs 82.61; 12 KiB 64 MiB 15.84 vs
+// 17.48, 128 MiB 28.88 / 28.12 vs 29.51 / 30.17, 256 MiB 46.01 / 45.68 vs 52.99 / 53.16, 512 MiB 90.06 / 89.33 vs
+// 93.73 / 93.18.  Outside that box it loses: 2 KiB and 6-7 KiB blocks at most sizes, 14-32 KiB blocks, 1 GiB.
+bool claim16_route(uint64_t count, uint64_t total_bytes, uint64_t max_len) {
+  const uint64_t bytes = total_bytes ? total_bytes : count * max_len;
+  return max_len >= 8 * 1024 && max_len <= 12 * 1024 && count >= 4096 && bytes <= (512ull << 20);
+}
+
 // Narrow-kernel form of a batch that use_narrow() put on the narrow kernels: 6 = 16-wave workgroups, 9 = 8-wave
 // workgroups (fill overlapped with the first loads), 10 = workgroup-contiguous runs dealt by LDS claims
-// (crc32c_narrow_claim_kernel, 8 waves), 20 = sorted windows (crc32c_narrow_sorted_kernel, 16 waves).
+// (crc32c_narrow_claim_kernel, 8 waves), 11 = the same with 16-lane slots, 20 = sorted windows
+// (crc32c_narrow_sorted_kernel, 16 waves).
 int narrow_form(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes, uint64_t max_len) {
   if (c->kernel == 3) return 6;
   if (c->kernel == 4) return 9;
   if (c->kernel == 5) return 20;
   if (c->kernel == 6) return 10;
+  if (c->kernel == 7) return 11;
   // 16-wave workgroups below 128 Ki blocks of <= 8 KiB (32 Ki blocks of 8-32 KiB), 8-wave ones from there on.  A
   // small batch gives each wave only a couple of 8-block groups, and more waves hide more of the launch/first-load
   // ramp (256 MiB of 4 KiB blocks: 16 waves +2-5 %); a large one streams better with 8 (1 GiB of 4 KiB blocks:
@@ -1947,6 +1963,7 @@ int narrow_form(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes,
   // sorting 64-block windows by length makes the groups even (config 4's 902 K blocks <= 32 KiB: 0.93 -> 0.57 ms
   // against the 16-wave narrow kernel, 1.24 ms on the 8-wave one).
   if (ragged_batch(count, total_bytes, max_len)) return 20;
+  if (claim16_route(count, total_bytes, max_len)) return 11;
   // The claim kernel (crc32c_narrow_claim_kernel) for uniform blocks of <= 8 KiB from 32 Ki of them up to 384 Ki of
   // <= 4 KiB (128 MiB - 1.5 GiB of 4 KiB blocks) or 64 Ki of 4-8 KiB.  Measured against both forms below in one
   // process (profiles/round4/queue_variants/claim_*.log, graph replay): 4 KiB blocks 128 MiB 26.8 vs 27.8 us, 256 MiB
@@ -1958,12 +1975,13 @@ int narrow_form(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes,
   return eight_waves ? 9 : 6;
 }
 
-bool use_narrow(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t max_len) {
+bool use_narrow(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes, uint64_t max_len) {
   if (max_len == 0 || max_len > 2 * kNarrowMax) return false;
   if (c->kernel == 1) return false;
   if (c->kernel >= 2) return true;
   const int d = diag_use_narrow(c);  // KVSEP_DIAG build only: -1 (no override) in the shipped library
   if (d >= 0) return d != 0;
+  if (claim16_route(count, total_bytes, max_len) && !ragged_batch(count, total_bytes, max_len)) return true;
   const uint64_t cus = uint64_t(c->num_cus);
   return (max_len <= 8 * 1024 && count >= 32 * cus) || (max_len <= 16 * 1024 && count >= 64 * cus) ||
          (max_len <= kNarrowMax && count >= 128 * cus);
@@ -2128,19 +2146,20 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     e1 = take_event(c);
     if (e0 && e1) KVSEP_HIP(hipEventRecord(e0, s));
   }
-  if (!planned && use_narrow(c, count, max_len)) {
+  if (!planned && use_narrow(c, count, total_bytes, max_len)) {
     int nv = narrow_form(c, count, total_bytes, max_len);
     nv = diag_narrow_form(c, nv);  // KVSEP_DIAG build only
     a.hint = max_len;
-    if (expect && (nv == 6 || nv == 9 || nv == 10 || nv == 20)) {  // the verify form of the shipped narrow forms
+    if (expect && (nv == 6 || nv == 9 || nv == 10 || nv == 11 || nv == 20)) {  // verify form of the shipped forms
       switch (nv) {
         case 9: crc32c_narrow_kernel<4, true, 512, true, 0, true, LdsFull, true><<<grid, 512, 0, s>>>(a); break;
         case 10: crc32c_narrow_claim_kernel<4, 512, true><<<grid, 512, 0, s>>>(a); break;
+        case 11: crc32c_narrow_claim_kernel<4, 512, true, true, 16><<<grid, 512, 0, s>>>(a); break;
         case 20: crc32c_narrow_sorted_kernel<4, true, 1024, false, 0, true><<<grid, 1024, 0, s>>>(a); break;
         default: crc32c_narrow_kernel<4, true, 1024, false, 0, true, LdsFull, true><<<grid, 1024, 0, s>>>(a); break;
       }
     } else {
-    // KVSEP_DIAG variants only (the shipped forms are 6, 9 and 20): they post to the caller's words directly, from
+    // KVSEP_DIAG variants only (the shipped forms are 6, 9, 10, 11 and 20): they post to the caller's words directly, from
     // their own in-kernel compare or from verify_finish_kernel, so those words are set first
     if (expect) {
       KVSEP_HIP(hipMemsetAsync(first_bad, 0xff, 8, s));
@@ -2151,6 +2170,7 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     switch (nv) {
       case 9: crc32c_narrow_kernel<4, true, 512, true><<<grid, 512, 0, s>>>(a); break;
       case 10: crc32c_narrow_claim_kernel<4, 512><<<grid, 512, 0, s>>>(a); break;
+      case 11: crc32c_narrow_claim_kernel<4, 512, false, true, 16><<<grid, 512, 0, s>>>(a); break;
       case 20: crc32c_narrow_sorted_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
       default: crc32c_narrow_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
     }
@@ -2270,7 +2290,7 @@ int kvsep_crc32c_ctx_set_schedule(kvsep_crc32c_ctx* c, int dynamic) {
 }
 
 int kvsep_crc32c_ctx_set_kernel(kvsep_crc32c_ctx* c, int kernel) {
-  if (!c || kernel < 0 || kernel > 6) return set_err(KVSEP_EINVAL, "kernel must be 0..6");
+  if (!c || kernel < 0 || kernel > 7) return set_err(KVSEP_EINVAL, "kernel must be 0..7");
   std::lock_guard<std::mutex> g(c->mu);
   c->kernel = kernel;
   return KVSEP_OK;
@@ -2404,9 +2424,10 @@ int kvsep_sst_verify_device(kvsep_crc32c_ctx* c, void* stream, const void* file_
 const char* kvsep_crc32c_kernel_name(kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes, uint64_t max_len) {
   if (!c) return "";
   const bool planned = !(max_len != 0 && max_len <= c->piece_bytes);
-  if (planned || !use_narrow(c, count, max_len)) return "crc32c_pieces_kernel";
+  if (planned || !use_narrow(c, count, total_bytes, max_len)) return "crc32c_pieces_kernel";
   const int nf = narrow_form(c, count, total_bytes, max_len);
-  return nf == 20 ? "crc32c_narrow_sorted_kernel" : nf == 10 ? "crc32c_narrow_claim_kernel" : "crc32c_narrow_kernel";
+  return nf == 20 ? "crc32c_narrow_sorted_kernel"
+         : nf == 10 || nf == 11 ? "crc32c_narrow_claim_kernel" : "crc32c_narrow_kernel";
 }
 
 int kvsep_stream_read_device(kvsep_crc32c_ctx* c, void* stream, const void* src, uint64_t nbytes, uint32_t* sink) {

@@ -685,13 +685,14 @@ class Workgroup:
             raise EmuError('sdwa modifier ' + k.text)
         t0, t1, td = self.SDWA_TMP
         if op.startswith('v_cmp_'):  # VOPC SDWA: the destination is an SGPR pair / VCC
-            m = re.match(r'v_cmp_(\w+)_([ui])16_sdwa$', op)
+            m = re.match(r'v_cmp_(\w+)_([ui])(16|32)_sdwa$', op)
             if not m:
                 raise EmuError('sdwa compare ' + k.text)
+            wide = m.group(3) == '32'  # a 32-bit compare of the (zero-extended, no sext) selected fields
             for i, (t, sel) in enumerate(zip(o[1:3], (k.mods.get('src0_sel'), k.mods.get('src1_sel')))):
-                w.v[(t0, t1)[i]] = sdwa_sel(w.vget(t), sel) & np.uint32(0xFFFF)
+                w.v[(t0, t1)[i]] = sdwa_sel(w.vget(t), sel) & np.uint32(0xFFFFFFFF if wide else 0xFFFF)
             plain = Insn(k.line, 'v_cmp_%s_%s32_e64 %s, v%d, v%d' % (m.group(1), m.group(2), o[0], t0, t1))
-            if m.group(2) == 'i':
+            if m.group(2) == 'i' and not wide:
                 for t in (t0, t1):
                     w.v[t] = (w.v[t].astype(np.uint16).view(np.int16).astype(np.int32)).view(np.uint32)
             return self.valu(w, plain, plain.op, plain.ops, act)

@@ -149,12 +149,17 @@ def test_sorted_windows_ragged(oracle, pool, count):
         assert ctx.kernel_name(n, 4096) == "crc32c_narrow_claim_kernel"  # total_bytes unknown: not ragged
         assert ctx.kernel_name(3 << 17, 4096, (3 << 17) * 4096) == "crc32c_narrow_claim_kernel"  # 1.5 GiB
         assert ctx.kernel_name(1 << 19, 4096, (1 << 19) * 4096) == "crc32c_narrow_kernel"  # 2 GiB and up: 8-wave
-        assert ctx.kernel_name(n, 16384, n * 16384) == "crc32c_narrow_kernel"  # blocks over 8 KiB
+        assert ctx.kernel_name(n, 16384, n * 16384) == "crc32c_narrow_kernel"  # blocks over 12 KiB
+        # 16-lane claim kernel (claim16_route): uniform 8-12 KiB blocks, >= 4 Ki of them, <= 512 MiB
+        assert ctx.kernel_name(6000, 10240, 6000 * 10240) == "crc32c_narrow_claim_kernel"  # was the wide kernel
+        assert ctx.kernel_name(3000, 10240, 3000 * 10240) == "crc32c_pieces_kernel"  # too few blocks
+        assert ctx.kernel_name(1 << 17, 8192, (1 << 17) * 8192) == "crc32c_narrow_kernel"  # 1 GiB
+        assert ctx.kernel_name(6000, 10240, 6000 * 4000) == "crc32c_pieces_kernel"  # ragged, too few for sorted
     finally:
         ctx.close()
 
 
-@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted", "claim"])
+@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted", "claim", "claim16"])
 @pytest.mark.parametrize("count", [70000, 200000])
 def test_verify_several_groups_per_wave(oracle, pool, kernel, count):
     """Verify form with several 8-block groups per wave (3 and 7 per 64-block window at these counts): the sorted
@@ -185,21 +190,23 @@ def test_verify_several_groups_per_wave(oracle, pool, kernel, count):
         ctx.close()
 
 
-@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted", "claim"])
+@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted", "claim", "claim16"])
 def test_every_end_geometry(oracle, pool, kernel):
     """Every case of the slot's end path: m = 0..7 whole 16-B chunks between the 128-B grid and the 16-B end (m = 7
-    uses all of lanes 0..6 of the tail load), each with head and tail bytes 0..15, with and without body rows."""
+    uses all of lanes 0..6 of the tail load), each with head and tail bytes 0..15, with and without body rows.  The
+    16-lane slots (claim16) have 256-B rows: m = 0..15 on the 256-B grid."""
     data, d = pool
     ctx = kvsep.Context(0)
     ctx.set_kernel(kernel)
+    row = 256 if kernel == "claim16" else 128
     ps, pe = [], []
     for rows in (-1, 0, 1, 3):  # -1: no row on the grid (a1 = h0 + 16 m)
-        for m in range(8):
+        for m in range(row // 16):
             for head in range(16):
                 for tail in (0, 1, 7, 15):
-                    start = 1024 * len(ps) + 16 + 128 - head  # ps % 16 == (16 - head) % 16: `head` head bytes
+                    start = 6 * row * len(ps) + 16 + row - head  # ps % 16 == (16 - head) % 16: `head` head bytes
                     h0 = start + head
-                    a1 = h0 + 16 * m if rows < 0 else ((h0 + 127) // 128 + rows) * 128 + 16 * m
+                    a1 = h0 + 16 * m if rows < 0 else ((h0 + row - 1) // row + rows) * row + 16 * m
                     ps.append(start)
                     pe.append(a1 + tail)
     off = np.array(ps, np.uint64)
@@ -211,7 +218,7 @@ def test_every_end_geometry(oracle, pool, kernel):
     assert np.array_equal(got, oracle.batch(data, off, ln, init))
 
 
-@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted", "claim"])
+@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted", "claim", "claim16"])
 def test_verify_mismatch_on_deferred_block(oracle, pool, kernel):
     """Verify form under an understated max_len: blocks longer than the hint leave their 8-block group and
     are checksummed by the deferred walk, whose compare is verify_uniform over the wave-uniform stored word.  Mismatches

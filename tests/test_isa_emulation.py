@@ -32,9 +32,10 @@ SORTED = "_ZN5kvsep27crc32c_narrow_sorted_kernelILi4ELb1ELi1024ELb0ELi0ELb%dEEEv
 NARROW16 = "_ZN5kvsep20crc32c_narrow_kernelILi4ELb1ELi1024ELb0ELi0ELb1ENS_7LdsFullELb%dEEEvNS_10PiecesArgsE"
 NARROW8 = "_ZN5kvsep20crc32c_narrow_kernelILi4ELb1ELi512ELb1ELi0ELb1ENS_7LdsFullELb%dEEEvNS_10PiecesArgsE"
 CLAIM = "_ZN5kvsep26crc32c_narrow_claim_kernelILi4ELi512ELb%dELb1ELi8EEEvNS_10PiecesArgsE"
+CLAIM16 = "_ZN5kvsep26crc32c_narrow_claim_kernelILi4ELi512ELb%dELb1ELi16EEEvNS_10PiecesArgsE"
 # (label, template, threads per workgroup, arrival levels of the verify publish: 8 = per-XCD shards, then the final word)
 KERNELS = [("sorted", SORTED, 1024, 1), ("narrow16", NARROW16, 1024, 1), ("narrow8", NARROW8, 512, 1),
-           ("claim", CLAIM, 512, 8)]
+           ("claim", CLAIM, 512, 8), ("claim16", CLAIM16, 512, 8)]
 
 
 @pytest.fixture(scope="module")
