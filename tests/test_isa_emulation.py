@@ -111,7 +111,7 @@ def _verify_tail(E, name, threads, data, off, ln, tabs, wg, hint, exp, mask, min
     assert st["vacc"] == (int(plant.min()), final, *sh), [hex(v) for v in st["vacc"]]
 
 
-PIECES = "_ZN5kvsep20crc32c_pieces_kernelILb%dELb%dELi4ELb1ELb1ELi0ELi512ELb1ELb%dEEEvNS_10PiecesArgsE"
+PIECES = "_ZN5kvsep20crc32c_pieces_kernelILb%dELb%dELi4ELb1ELb1ELi0ELi512ELb1ELb%dELi0EEEvNS_10PiecesArgsE"
 COMBINE = "_ZN5kvsep21crc32c_combine_kernelILb%dEEEvNS_10PiecesArgsE"
 
 
