@@ -290,9 +290,25 @@ def cpu_baseline(oracle, data_dev, off, ln, sample_blocks, thread_counts, second
     return out, host, hoff, lens, idx, kind
 
 
-def sse42_rate(host, hoff, lens, threads, seconds):
-    """Informational: the library's own SSE4.2 `crc32` host leg (the drop-in's small-input path, i.e. the
-    "accelerated" CPU path google/crc32c would give the reference) over the same host sample; GiB/s."""
+def host_leg_path() -> str:
+    """Which host leg kvsep_crc32c_extend_host runs here (crc32c_host.cpp fold_available): the VPCLMULQDQ fold on
+    CPUs with AVX-512F + VPCLMULQDQ (unless KVSEP_HOST_CRC=sse42), else the SSE4.2 3-way crc32q loop."""
+    flags = set()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("flags"):
+                flags = set(line.split(":", 1)[1].split())
+                break
+    except OSError:
+        pass
+    fold = {"avx512f", "vpclmulqdq", "pclmulqdq", "sse4_2"} <= flags and os.environ.get("KVSEP_HOST_CRC") != "sse42"
+    return ("VPCLMULQDQ fold (4 x 512-bit accumulators, 256 B per round) + crc32q tail" if fold
+            else "SSE4.2 crc32q, 3-way interleaved")
+
+
+def host_leg_rate(host, hoff, lens, threads, seconds):
+    """Informational: the library's own host leg (the drop-in's small-input path, i.e. the "accelerated" CPU path
+    google/crc32c would give the reference) over the same host sample; GiB/s."""
     fn = kvsep.lib().kvsep_crc32c_extend_host
     base = host.ctypes.data
     items = [(base + int(o), int(n)) for o, n in zip(hoff, lens)]
@@ -736,12 +752,12 @@ def main():
                    "limit_note": (f"this process may use {quota:g} CPUs' worth of time (cgroup cpu.max) of the {aff} "
                                   f"it may run on: rates flatten from {int(quota)} threads on" if quota and quota < aff
                                   else "no cgroup CPU limit below the affinity set")}
-            s1 = sse42_rate(host, hoff[:max(1, nsample // 4)], lens[:max(1, nsample // 4)], 1, 2.0)
-            sn = sse42_rate(host, hoff, lens, threads, 2.0)
-            cpu["sse42_crc32_GiBps"] = {"1": round(s1, 3), str(threads): round(sn, 3),
-                                        "note": "informational, not the baseline: the library's SSE4.2 crc32 host "
-                                                "leg (3-way interleaved crc32q) on the same sample; the reference "
-                                                "build here has no accelerated path (HAVE_CRC32C=0)"}
+            s1 = host_leg_rate(host, hoff[:max(1, nsample // 4)], lens[:max(1, nsample // 4)], 1, 2.0)
+            sn = host_leg_rate(host, hoff, lens, threads, 2.0)
+            cpu["host_leg_GiBps"] = {"1": round(s1, 3), str(threads): round(sn, 3), "path": host_leg_path(),
+                                     "note": "informational, not the baseline: the library's own host leg (the "
+                                             "drop-in's small-input path) on the same sample; the reference build "
+                                             "here has no accelerated path (HAVE_CRC32C=0)"}
 
     # host round trip (PCIe-inclusive).  At N > 1 every rank streams its own pinned image through its own GPU
     # at the same time (each GPU has its own PCIe link); the rate is the sum over ranks / the slowest rank.

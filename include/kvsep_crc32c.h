@@ -44,8 +44,8 @@ int kvsep_abi_version(void);
  * Same contract as util/crc32c.h:17 / util/crc32c.cc:276: CRC-32C of A||data[0,n) where
  * init_crc = crc32c(A); n == 0 returns init_crc; any alignment; never fails; reentrant.
  * Dispatch: n >= the offload threshold (kvsep_set_offload_threshold, default 64 MiB) goes through
- * the GPU (pinned staging, H2D, kernel, D2H); smaller inputs use the host SSE4.2 path
- * (the role google/crc32c plays behind port::AcceleratedCRC32C). */
+ * the GPU (pinned staging, H2D, kernel, D2H); smaller inputs use the host leg (VPCLMULQDQ folding on CPUs with
+ * AVX-512 carry-less multiply, else SSE4.2 crc32 -- the role google/crc32c plays behind port::AcceleratedCRC32C). */
 uint32_t kvsep_crc32c_extend(uint32_t init_crc, const char* data, size_t n);
 uint32_t kvsep_crc32c_value(const char* data, size_t n); /* util/crc32c.h:20 */
 uint32_t kvsep_crc32c_mask(uint32_t crc);                /* util/crc32c.h:29-32 */
@@ -58,12 +58,13 @@ void kvsep_set_offload_threshold(uint64_t nbytes);
  * compaction, GC and reader threads concurrently (db/db_impl.cc:1829-1833), and one PCIe link serves one
  * staged copy at a time while every core can run the host leg. */
 void kvsep_set_offload_wait(int wait);
-/* Counters of the scalar drop-in since load (any may be null): calls served by the GPU, calls served by
- * the host path (below the threshold, or diverted because the GPU leg was busy), and calls at/above the
- * threshold that the GPU could not serve and that finished on the host (set KVSEP_STRICT_GPU=1 to abort on
- * those instead). */
+/* Counters of the scalar drop-in's calls at/above the offload threshold since load (any may be null): calls
+ * served by the GPU, calls diverted to the host leg because the GPU leg was busy, and calls that the GPU could
+ * not serve and that finished on the host (set KVSEP_STRICT_GPU=1 to abort on those instead).  Calls below the
+ * threshold are not counted (no shared counter on the small-call path). */
 void kvsep_offload_stats(uint64_t* gpu_calls, uint64_t* host_calls, uint64_t* gpu_failures);
-/* Host-only CRC (SSE4.2 crc32 instructions, 3-way interleaved): the small-input leg of Extend. */
+/* Host-only CRC, the small-input leg of Extend: VPCLMULQDQ folding (4 x 512-bit accumulators) where the CPU has
+ * AVX-512F + VPCLMULQDQ, else SSE4.2 crc32 3-way interleaved (KVSEP_HOST_CRC=sse42 forces the latter). */
 uint32_t kvsep_crc32c_extend_host(uint32_t init_crc, const char* data, size_t n);
 
 /* ---------------------------------------------------------------- device context */

@@ -6,7 +6,9 @@ db_bench --benchmarks=crc32c (benchmarks/db_bench.cc:693-710) checksums 4 KiB of
   reference   oracle/_ref/dbbench_crc32c_ref: that loop (tools/dbbench_crc32c.cc) linked with the reference's
               util/crc32c.cc (portable path, -O3) -- what db_bench prints for this fork on this host
   drop-in     tools/dbbench_crc32c_kvsep: the same loop linked with libkvsep_leveldb_abi.so, i.e. the link-level
-              drop-in; a 4 KiB Extend runs on the library's SSE4.2 host leg (a single call cannot win on the GPU)
+              drop-in; a 4 KiB Extend runs on the library's host leg (a single call cannot win on the GPU): the
+              VPCLMULQDQ fold where the CPU has it ("dropin"), and the SSE4.2 crc32q loop (KVSEP_HOST_CRC=sse42,
+              "dropin_sse42")
   device      the same 128,000 blocks as ONE batched call (kvsep_crc32c_batch_device): 500 MiB of 'x' resident in
               HBM, 128,000 descriptors, the north star's block batch; K calls captured into one hipGraph, HIP events
   host batch  the same 128,000 blocks from a pinned host buffer (kvsep_crc32c_batch_host_span: H2D + kernel + D2H)
@@ -32,10 +34,11 @@ OPS = TOTAL // SIZE
 MB = 1048576.0
 
 
-def run_binary(path, reps):
+def run_binary(path, reps, env=None):
     if not os.path.exists(path):
         return None
-    lines = subprocess.run([path, str(reps)], capture_output=True, text=True, check=True, timeout=600).stdout
+    lines = subprocess.run([path, str(reps)], capture_output=True, text=True, check=True, timeout=600,
+                           env=dict(os.environ, **(env or {}))).stdout
     runs = [json.loads(l) for l in lines.splitlines() if l.startswith("{")]
     return {"MBps_median": round(statistics.median(r["MBps"] for r in runs), 1),
             "MBps_runs": [r["MBps"] for r in runs], "crc": runs[0]["crc"], "ops": runs[0]["ops"],
@@ -50,8 +53,12 @@ def main():
     out = {"convention": "db_bench --benchmarks=crc32c: 4 KiB of 'x', Value repeated to 500 MiB (128,000 calls), "
                          "MB/s with MB = 2^20 (benchmarks/db_bench.cc:693-710, :320-321)"}
     out["reference"] = run_binary(os.path.join(ROOT, "oracle", "_ref", "dbbench_crc32c_ref"), args.reps)
-    out["dropin_sse42"] = run_binary(os.path.join(HERE, "dbbench_crc32c_kvsep"), args.reps)
-    want = int((out["reference"] or out["dropin_sse42"])["crc"], 16)
+    out["dropin"] = run_binary(os.path.join(HERE, "dbbench_crc32c_kvsep"), args.reps)
+    out["dropin_sse42"] = run_binary(os.path.join(HERE, "dbbench_crc32c_kvsep"), args.reps, {"KVSEP_HOST_CRC": "sse42"})
+    want = int((out["reference"] or out["dropin"])["crc"], 16)
+    for k in ("dropin", "dropin_sse42"):
+        if out[k]:
+            out[k]["crc_equals_reference"] = int(out[k]["crc"], 16) == want
 
     dev = torch.device("cuda:0")
     ctx = kvsep.Context(0)

@@ -52,11 +52,12 @@ def test_abi_version():
 
 def test_no_environment_variable_reaches_the_kernel_choice():
     """The shipped library reads no variant / kernel-routing variable (those exist only in the KVSEP_DIAG tools
-    build): only KVSEP_STRICT_GPU and KVSEP_COPY_THREADS, neither of which can change a CRC."""
+    build): only KVSEP_STRICT_GPU, KVSEP_COPY_THREADS and KVSEP_HOST_CRC (=sse42: the host leg's crc32 loop instead of
+    the VPCLMULQDQ fold, for A/B), none of which can change a CRC."""
     import re
     strings = open(kvsep.LIB_PATH, "rb").read()
     names = set(re.findall(rb"KVSEP_[A-Z_]{3,}", strings))
-    assert names <= {b"KVSEP_STRICT_GPU", b"KVSEP_COPY_THREADS"}, names
+    assert names <= {b"KVSEP_STRICT_GPU", b"KVSEP_COPY_THREADS", b"KVSEP_HOST_CRC"}, names
 
 
 def test_python_extend_rejects_n_past_buffer():
@@ -156,3 +157,34 @@ def test_host_extend_lane_boundaries(oracle):
             for init in (0, 0x9E3779B9):
                 b = data[o:o + n].tobytes()
                 assert f(init, data.ctypes.data + o, n) == oracle.extend(init, b), (o, n, init)
+
+
+def test_host_extend_fold_boundaries(oracle):
+    """The host leg's VPCLMULQDQ fold (crc32c_host.cpp fold_bulk) takes whole 256-B rounds and leaves the rest to the
+    crc32 loop: every length around 256 k for k = 1..9, at 64 start offsets (the zmm loads' alignments) and three
+    inits, against the oracle.  On a CPU without AVX-512 VPCLMULQDQ this runs the crc32 path (exact either way)."""
+    data = splitmix64_bytes(8192, 91, 0)
+    f = kvsep.lib().kvsep_crc32c_extend_host
+    lens = sorted({n for k in range(1, 10) for n in range(256 * k - 5, 256 * k + 21)} | {4096, 4097, 4095})
+    for o in range(64):
+        for n in lens:
+            b = data[o:o + n].tobytes()
+            for init in (0, 0xFFFFFFFF, 0x9E3779B9 ^ o):
+                assert f(init, data.ctypes.data + o, n) == oracle.extend(init, b), (o, n, init)
+
+
+def test_host_extend_both_paths_in_subprocess():
+    """KVSEP_HOST_CRC=sse42 keeps the crc32 3-way loop (the path of CPUs without AVX-512 VPCLMULQDQ): run the lane
+    boundary and fold boundary sweeps in a child process with it set, so that path stays covered on this machine."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, KVSEP_HOST_CRC="sse42")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
+                        os.path.join(here, "test_abi_cpu.py") + "::test_host_extend_lane_boundaries",
+                        os.path.join(here, "test_abi_cpu.py") + "::test_host_extend_fold_boundaries",
+                        os.path.join(here, "test_abi_cpu.py") + "::test_host_extend_large"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert "3 passed" in r.stdout, r.stdout[-2000:]
