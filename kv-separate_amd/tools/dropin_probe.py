@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Where should the scalar drop-in (kvsep_crc32c_extend, the util/crc32c.h:17 replacement) hand a single buffer
-to the GPU?  Times one Extend over a pageable buffer of each size on the host SSE4.2 leg and through the GPU
+to the GPU?  Times one Extend over a pageable buffer of each size on the host leg and through the GPU
 (threshold forced to 0), single caller and with 8 concurrent callers (the reference calls Extend from the
 writer, compaction, GC and reader threads at once, db/db_impl.cc:1829-1833).  Prints one line per size."""
 import json
