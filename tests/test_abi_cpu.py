@@ -160,14 +160,15 @@ def test_host_extend_lane_boundaries(oracle):
 
 
 def test_host_extend_fold_boundaries(oracle):
-    """The host leg's VPCLMULQDQ fold (crc32c_host.cpp fold_bulk) takes whole 256-B rounds, then the remainder's
-    64-B and 16-B chunks, and leaves < 16 B to the crc32 loop: every length around 256 k for k = 1..9 at 64 start
-    offsets (the zmm loads' alignments), and every length 256..1023 (every remainder) at 8 offsets, three inits each,
+    """The host leg's VPCLMULQDQ fold (crc32c_host.cpp fold_bulk, from 128 B) takes whole 256-B rounds, then the
+    remainder's 64-B and 16-B chunks, and leaves < 16 B to the crc32 loop: every length around 256 k for k = 1..9 at
+    64 start offsets (the zmm loads' alignments), and every length 0..1023 (both entries, every remainder) at 8
+    offsets, three inits each,
     against the oracle.  On a CPU without AVX-512 VPCLMULQDQ this runs the crc32 path (exact either way)."""
     data = splitmix64_bytes(8192, 91, 0)
     f = kvsep.lib().kvsep_crc32c_extend_host
     lens = sorted({n for k in range(1, 10) for n in range(256 * k - 5, 256 * k + 21)} | {4096, 4097, 4095})
-    cases = [(o, n) for o in range(64) for n in lens] + [(o, n) for o in range(0, 64, 9) for n in range(256, 1024)]
+    cases = [(o, n) for o in range(64) for n in lens] + [(o, n) for o in range(0, 64, 9) for n in range(0, 1024)]
     for o, n in cases:
         b = data[o:o + n].tobytes()
         for init in (0, 0xFFFFFFFF, 0x9E3779B9 ^ o):
