@@ -248,7 +248,44 @@ def spread_cpus(allowed):
     return order, node_of
 
 
-def cpu_baseline(oracle, data_dev, off, ln, sample_blocks, thread_counts, seconds):
+def place_rank(device: int, mode: str) -> dict:
+    """NUMA placement of this rank's host legs (round 5): every thread of the process onto the CPUs of the NUMA node of
+    its GPU's PCI function, and that node the main thread's preferred memory node, so the pinned round-trip image and
+    the library's pinned staging (which its context also places there, kvsep_crc32c_ctx_set_host_node) sit next to
+    the GPU's PCIe root.  Called right after selecting the device and before any pinned allocation; an affinity call
+    in this process, never a re-exec.  -> what was done, for the line."""
+    info = {"numa_node": None, "bound_cpus": 0, "mode": mode}
+    try:
+        info["numa_node"] = kvsep.device_numa_node(device)
+        if mode != "off" and info["numa_node"] is not None and info["numa_node"] >= 0:
+            info["bound_cpus"] = kvsep.bind_process_numa(info["numa_node"])
+    except Exception as e:  # placement is an optimisation: the line never depends on it
+        info["error"] = str(e)[:200]
+    return info
+
+
+def rank_record(rank, local, device, placement, kern_avg_ms, own_s, t_start, t_end, nbytes, kernel_name,
+                launch_bytes=0):
+    """This rank's entry of the line's `per_rank`: which physical GPU (PCI bus ID), where its host legs run (NUMA node,
+    CPU affinity), and its own timing -- kernel time by HIP events, elapsed from the start barrier to its own last
+    synchronize (before the end barrier), the GiB/s that gives, and wall-clock start / end stamps (one host clock)."""
+    rec = {"rank": rank, "local_rank": local, "device": device, "pid": os.getpid(),
+           "pci_bus_id": None, "numa_node": placement.get("numa_node"), "bound_cpus": placement.get("bound_cpus"),
+           "cpu_affinity": kvsep.format_cpulist(os.sched_getaffinity(0)),
+           "kernel": kernel_name, "kernel_avg_ms": None if kern_avg_ms is None else round(kern_avg_ms, 5),
+           "elapsed_s": None if own_s is None else round(own_s, 6),
+           "GiBps": None if not own_s else round(nbytes / GIB / own_s, 3),
+           "kernel_GBps": round(launch_bytes / (kern_avg_ms * 1e-3) / 1e9, 1) if kern_avg_ms and launch_bytes else None,
+           "t_start": t_start, "t_end": t_end}
+    if device is not None:
+        try:
+            rec["pci_bus_id"] = kvsep.pci_bus_id(device)
+        except Exception as e:
+            rec["pci_bus_id_error"] = str(e)[:120]
+    return rec
+
+
+def cpu_baseline(oracle, data_dev, off, ln, sample_blocks, thread_counts, seconds, allowed=None):
     """CPU CRC on host cores over a sample of the batch: the compiled reference (kind "reference") when oracle/_ref
     was built, else the oracle restatement (kind "port"), at each thread count in `thread_counts`.  The reference runs
     through ref_crc32c_timed_local: threads pinned spread over the NUMA nodes (spread_cpus), each checksumming its own
@@ -267,7 +304,7 @@ def cpu_baseline(oracle, data_dev, off, ln, sample_blocks, thread_counts, second
     impl, kind = oracle, "port"
     if os.path.exists(RefBatch.PATH):
         impl, kind = RefBatch(), "reference"
-        order, node_of = spread_cpus(os.sched_getaffinity(0))
+        order, node_of = spread_cpus(allowed or os.sched_getaffinity(0))
         impl.batch(host, hoff[:8], lens[:8], threads=1)  # warm tables
         for t in thread_counts:
             cpus = order[:t] if t <= len(order) else (order * (t // len(order) + 1))[:t]
@@ -506,6 +543,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="CPU work per thread count (>= 1 pass)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--roundtrip-gib", type=float, default=4.0)
+    ap.add_argument("--numa-bind", default="auto", choices=["auto", "off"],
+                    help="auto: bind each rank's threads (and its pinned memory) to its GPU's NUMA node (place_rank)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: each rank joins a gloo group, the ranks agree on the world "
                          "size and rank 0 prints a JSON line with n_gpus / backend (tests/test_bench_launch.py)")
@@ -538,9 +577,15 @@ def main():
             dist.all_gather(seen, t)
             ranks = sorted(int(x[1]) for x in seen)
             assert ranks == list(range(world)) and all(int(x[0]) == world for x in seen), seen
+        # the per-rank records travel the same way as on the GPU path (no device: no bus ID, no kernel)
+        t_start = time.time()
+        rec = rank_record(rank, local, None, {"numa_node": None, "bound_cpus": 0}, None, 1.0, t_start, time.time(),
+                          GIB, None)
+        per_rank = shard.gather_objects(rec, dist if world > 1 else None)
         if rank == 0:
             print(json.dumps({"dry_run": True, "n_gpus": world, "world_size": world,
-                              "backend": dist.get_backend() if world > 1 else None}), flush=True)
+                              "backend": dist.get_backend() if world > 1 else None, "per_rank": per_rank,
+                              "per_rank_summary": shard.rank_summary(per_rank, same_device=False)}), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -559,6 +604,9 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     coll_dev = dev if dd is None or dist.get_backend() == "nccl" else torch.device("cpu")
+    allowed_cpus = os.sched_getaffinity(0)  # before placement: the CPU baseline spreads over every node
+    placement = place_rank(local, args.numa_bind)
+    same_device = bool(os.environ.get("KVSEP_BENCH_SAME_DEVICE"))
 
     ctx = kvsep.Context(local)
     if args.piece_kib:
@@ -638,6 +686,7 @@ def main():
         if dd:
             dist.barrier()
         torch.cuda.synchronize()
+        t_start = time.time()
         t0 = time.perf_counter()
         if span_timing:
             ev[0].record()  # the graph replays on the current stream
@@ -646,6 +695,8 @@ def main():
         if span_timing:
             ev[1].record()
         torch.cuda.synchronize()
+        own = time.perf_counter() - t0  # this rank's own time, before waiting for the others
+        t_end = time.time()
         if dd:
             dist.barrier()
         elapsed = time.perf_counter() - t0
@@ -660,7 +711,8 @@ def main():
         # pass's slice is (re)generated in HBM before its timed region opens -- the data "arriving" -- so every
         # timed pass starts with its input resident, like every other config; each pass is bracketed by barrier +
         # synchronize, the step time is the sum of its passes.
-        elapsed = 0.0
+        elapsed = own = 0.0
+        t_start = t_end = None
         ctx.get_timing()
         for _ in range(args.steps):
             for p in range(npass):
@@ -669,9 +721,12 @@ def main():
                 if dd:
                     dist.barrier()
                 ctx.set_timing(True)
+                t_start = time.time() if t_start is None else t_start
                 t0 = time.perf_counter()
                 crc(p, stream)
                 torch.cuda.synchronize()
+                own += time.perf_counter() - t0
+                t_end = time.time()
                 if dd:
                     dist.barrier()
                 elapsed += time.perf_counter() - t0
@@ -687,6 +742,8 @@ def main():
     kern_avg_ms = kern_ms / max(1, launches)
     kernel_name = ctx.kernel_name(count, max_len, useful)
     achieved_gbps = useful / (kern_avg_ms * 1e-3) / 1e9
+    my_record = rank_record(rank, local, local, placement, kern_avg_ms, own, t_start, t_end,
+                            useful * npass * args.steps, kernel_name, launch_bytes=useful)
 
     # ---- outside the timed region: u32 results of every rank gathered (RCCL), every block checked
     crcs = out[:, :count].cpu().numpy().view(np.uint32).reshape(-1)
@@ -714,7 +771,7 @@ def main():
         parity["all_blocks_match"] = parity["mismatches"] == 0 and parity["mismatching_digest_ranges"] == 0
         res = None
         if not args.no_cpu and world == 1:
-            aff = len(os.sched_getaffinity(0))
+            aff = len(allowed_cpus)
             most = args.cpu_threads or aff
             quota_raw, quota = cpu_quota()
             counts = {1, most} | {t for t in (8, 16, 32, 64, 128) if t < most}
@@ -724,7 +781,7 @@ def main():
             nsample = min(args.cpu_sample_blocks, count)
             try:
                 res, host, hoff, lens, idx, kind = cpu_baseline(oracle, data, off, ln, nsample, counts,
-                                                                args.cpu_seconds)
+                                                                args.cpu_seconds, allowed=allowed_cpus)
             except Exception as e:  # the headline line never depends on the CPU leg
                 log(f"[rank 0] cpu baseline failed: {e}")
                 res = None
@@ -778,11 +835,23 @@ def main():
                 dt, good = roundtrip_time(ctx, state)
             except Exception as e:
                 log(f"[rank {rank}] host round trip failed: {e}")
+            if dt != float("inf"):
+                my_record["roundtrip_GiBps"] = round(float(state[3].sum()) / GIB / dt, 3)
+                my_record["roundtrip_image_numa_node"] = kvsep.host_page_node(state[0].data_ptr())
             dt = shard.max_over_ranks(dt, dd, coll_dev)
             rt_ok = bool(shard.min_over_ranks(1 if good else 0, dd, coll_dev))
             if dt != float("inf"):
                 rt = round(world * float(state[3].sum()) / GIB / dt, 3)
         state = None
+    # every rank's record (bus ID, NUMA node, affinity, its own kernel time / elapsed / GiB/s, its host staging), so
+    # an N-rank line can tell one slow GPU from launch skew or a shared-host effect
+    try:
+        st = ctx.host_placement()
+        st["copier_cpus"] = kvsep.format_cpulist(st["copier_cpus"])
+        my_record["staging"] = st
+    except Exception:
+        pass
+    per_rank = shard.gather_objects(my_record, dd)
 
     traffic = None
     traffic_src = None
@@ -850,6 +919,8 @@ def main():
             "parity": parity,
             "parity_spot_check": bool(parity and parity["all_blocks_match"]),
             "digests": [hex(d) for d in digests],
+            "per_rank": per_rank,
+            "per_rank_summary": shard.rank_summary(per_rank, same_device=same_device),
         }
         print(json.dumps(line), flush=True)
     ctx.close()

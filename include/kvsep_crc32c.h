@@ -29,9 +29,12 @@ extern "C" {
 
 /* ABI version.  2 (round 3): kvsep_vlog_verify_host takes *drop_bytes (7 arguments) and kvsep_crc32c_kernel_name
  * takes total_bytes before max_len -- both changed in place from ABI 1, so a caller built against ABI 1 must be
- * rebuilt; check kvsep_abi_version() == KVSEP_ABI_VERSION once at startup.  The reference's C++ symbol
- * leveldb::crc32c::Extend is not in this library: it is in the libkvsep_leveldb_abi.so shim. */
-#define KVSEP_ABI_VERSION 2
+ * rebuilt; check kvsep_abi_version() == KVSEP_ABI_VERSION once at startup.  3 (round 5): kvsep_offload_stats counts
+ * only calls at or above the offload threshold (since round 4: host_calls no longer includes the calls below it, which
+ * are not counted at all); new entry points for the host legs, topology and host placement; no signature changed.
+ * The reference's C++ symbol leveldb::crc32c::Extend is not in this library: it is in the libkvsep_leveldb_abi.so
+ * shim. */
+#define KVSEP_ABI_VERSION 3
 int kvsep_abi_version(void);
 
 #define KVSEP_OK 0
@@ -63,9 +66,13 @@ void kvsep_set_offload_wait(int wait);
  * not serve and that finished on the host (set KVSEP_STRICT_GPU=1 to abort on those instead).  Calls below the
  * threshold are not counted (no shared counter on the small-call path). */
 void kvsep_offload_stats(uint64_t* gpu_calls, uint64_t* host_calls, uint64_t* gpu_failures);
-/* Host-only CRC, the small-input leg of Extend: VPCLMULQDQ folding (4 x 512-bit accumulators) where the CPU has
- * AVX-512F + VPCLMULQDQ, else SSE4.2 crc32 3-way interleaved (KVSEP_HOST_CRC=sse42 forces the latter). */
+/* Host-only CRC, the small-input leg of Extend, on the fastest leg this CPU runs (checked once, at first use):
+ * "fold" (x86-64 with AVX-512F + VPCLMULQDQ: 4 x 512-bit accumulators), else "sse42" (x86-64 with SSE4.2: the crc32
+ * instruction, 3-way interleaved), else "portable" (any CPU: table-driven, slicing-by-8).  KVSEP_HOST_CRC=sse42 or
+ * =portable forces a slower leg.  Exact on every leg; never an illegal instruction on a CPU without the extension. */
 uint32_t kvsep_crc32c_extend_host(uint32_t init_crc, const char* data, size_t n);
+/* The leg kvsep_crc32c_extend_host runs in this process: "fold", "sse42" or "portable". */
+const char* kvsep_crc32c_host_path(void);
 
 /* ---------------------------------------------------------------- device context */
 typedef struct kvsep_crc32c_ctx kvsep_crc32c_ctx;
@@ -85,6 +92,19 @@ int kvsep_crc32c_ctx_set_schedule(kvsep_crc32c_ctx* ctx, int dynamic);
  * 16 lanes per block, 4-block groups (auto: uniform batches of >= 4 Ki blocks of 8-12 KiB, up to 512 MiB).
  * A choice of speed only: every kernel is exact for every block.  No environment variable changes it. */
 int kvsep_crc32c_ctx_set_kernel(kvsep_crc32c_ctx* ctx, int kernel);
+/* NUMA node the context's host legs are placed on: its pinned staging is allocated, and its copier threads run, on
+ * the CPUs of this node that the allocating thread may use.  Default: the node of the device's PCI function
+ * (kvsep_device_numa_node); -1 = no placement.  Takes effect for staging not yet allocated (set it before the first
+ * host-form call).  The group forms also bind each member's host thread to its member's node for the call. */
+int kvsep_crc32c_ctx_set_host_node(kvsep_crc32c_ctx* ctx, int node);
+/* Where the context's host legs are: *device_node = the node it places them on (-1: none), *staging_node = the node
+ * holding its first pinned staging slot (-1: not allocated yet / unknown), cpus[0..cap) = the CPUs its copier threads
+ * are bound to.  Returns the number of those CPUs (0: not bound), or KVSEP_EINVAL. */
+int kvsep_crc32c_ctx_host_placement(kvsep_crc32c_ctx* ctx, int* device_node, int* staging_node, int* cpus, int cap);
+/* Fault injection (tests): the context's next batched call returns KVSEP_EHIP right after it enqueued its CRC kernel,
+ * before the combine kernel of a planned batch -- the one point where a verify call's accumulators hold posts that no
+ * kernel will publish.  The next verify call on the context resets them first, so its verdict is exact. */
+int kvsep_crc32c_ctx_inject_failure(kvsep_crc32c_ctx* ctx);
 /* Pre-size scratch so later calls of up to `count` blocks / `total_bytes` bytes do not allocate
  * (required before graph capture; covers the planned, narrow, verify and SST-verify forms). */
 int kvsep_crc32c_reserve(kvsep_crc32c_ctx* ctx, uint64_t count, uint64_t total_bytes);
@@ -229,6 +249,25 @@ int kvsep_crc32c_group_verify_device(kvsep_crc32c_group* g, const void* const* b
                                      const uint32_t* const* expected_masked, uint32_t* const* out,
                                      const uint64_t* index_base, const uint64_t* count, const uint64_t* total_bytes,
                                      const uint64_t* max_len, uint64_t* first_bad, uint64_t* nbad);
+
+/* ---------------------------------------------------------------- topology and host placement (round 5)
+ * Which physical GPU a caller runs on, and the NUMA node its host legs belong on.  sysfs is read under
+ * $KVSEP_SYSFS_ROOT (default /sys). */
+/* PCI bus ID of a device ("0000:75:00.0", lower case, as sysfs spells it) into buf (len >= 13). */
+int kvsep_device_pci_bus_id(int device, char* buf, int len);
+/* NUMA node of a PCI function / of a device (sysfs numa_node), -1 when unknown. */
+int kvsep_pci_numa_node(const char* pci_bus_id);
+int kvsep_device_numa_node(int device);
+/* CPUs of a NUMA node (sysfs cpulist) into cpus[0..cap); returns how many it has (0: unknown node). */
+int kvsep_numa_node_cpus(int node, int* cpus, int cap);
+/* Binds every thread of the calling process to the CPUs of `node` that the calling thread may run on, and makes
+ * `node` the calling thread's preferred memory node (its later allocations, pinned host buffers included, land there
+ * first).  Returns the number of CPUs bound to; 0 (nothing changed) for an unknown node or one that shares no CPU
+ * with the current affinity.  For a process that drives one GPU (a bench rank): call it right after selecting the
+ * device, before allocating pinned memory. */
+int kvsep_bind_process_numa(int node);
+/* NUMA node of the page holding p (faulted in if never touched), -1 if unknown. */
+int kvsep_host_page_node(const void* p);
 
 /* Pinned (page-locked) host memory for file images: read a vlog / SST file straight into it and the
  * host-span entry points DMA from it directly, without the staging memcpy.  NULL on failure. */

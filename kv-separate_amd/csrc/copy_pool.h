@@ -2,6 +2,9 @@
 // ThreadSanitizer and AddressSanitizer).  Persistent threads copy pageable data into the pinned staging slots in
 // parallel: one thread's memcpy (~10-25 GB/s) is below the PCIe Gen5 x16 rate the slots are drained at (~55 GB/s).
 #pragma once
+#include <pthread.h>
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
@@ -23,7 +26,8 @@ struct CopySeg {
 
 class CopyPool {
  public:
-  explicit CopyPool(int nthreads) {
+  // cpus: the CPUs the workers run on (the staged device's NUMA node), or empty for the creator's affinity.
+  explicit CopyPool(int nthreads, std::vector<int> cpus = {}) : cpus_(std::move(cpus)) {
     for (int i = 0; i < nthreads; ++i) th_.emplace_back([this] { worker(); });
   }
   ~CopyPool() {
@@ -88,6 +92,14 @@ class CopyPool {
       for (uint64_t c = units_[k].first; c < units_[k].second; ++c) copy(chunks_[c]);
   }
   void worker() {
+    pthread_setname_np(pthread_self(), "kvsep-copy");
+    if (!cpus_.empty()) {
+      cpu_set_t s;
+      CPU_ZERO(&s);
+      for (int c : cpus_)
+        if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &s);
+      (void)sched_setaffinity(0, sizeof s, &s);
+    }
     uint64_t seen = 0;
     for (;;) {
       {
@@ -101,6 +113,7 @@ class CopyPool {
       if (--active_ == 0) done_cv_.notify_one();
     }
   }
+  const std::vector<int> cpus_;
   std::vector<std::thread> th_;
   std::vector<CopySeg> chunks_;
   std::vector<std::pair<uint64_t, uint64_t>> units_;  // [first, end) chunk ranges claimed as one

@@ -1786,6 +1786,8 @@ struct kvsep_crc32c_ctx {
   int variant = 1;   // KVSEP_DIAG builds only: A/B and ablation variants of the wide kernel (launch_pieces_v)
   int narrow = 1;    // KVSEP_DIAG builds only: narrow-kernel variants
   Scratch sc;  // scratch of the calls made directly on this context (any stream, event-ordered)
+  int host_node = -1;        // NUMA node of the device's PCI function (-1: unknown / not bound): host legs go there
+  bool inject_failure = false;  // kvsep_crc32c_ctx_inject_failure: the next call fails right after its CRC kernel
   // timing
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
@@ -1865,16 +1867,34 @@ int release(Scratch& sc, hipStream_t s) {
 }
 
 // The verify form's device words (allocated once per scratch, before any capture -- kvsep_crc32c_reserve does it): on
-// the first 128-B line the result words of a call whose caller passes none; then the accumulators the kernels post to
-// and reset (PiecesArgs::vacc: the lowest-block word and the final arrival word, then 8 shard arrival words, each group
-// on a line of its own), which must start in their reset state: ~0 (no mismatch), 0 (nothing arrived, none bad).
+// the first 128-B line the result words of a call whose caller passes none; then kVaccLines sets of the accumulators
+// the kernels post to and reset (PiecesArgs::vacc: the lowest-block word and the final arrival word, then 8 shard
+// arrival words, each group on a line of its own), which must start in their reset state: ~0 (no mismatch), 0
+// (nothing arrived, none bad).  Set 0 serves eager calls, which the scratch's events order one after another; each
+// captured call takes one of the other sets in turn, so replays of up to kVaccLines - 1 captured verify calls may
+// overlap (two graphs on two streams) without mixing their arrivals.
+constexpr uint32_t kVaccLines = 8, kVaccSetWords = kVaccStride * (1 + kVaccShards);
+unsigned long long* vacc_set(Scratch& sc, uint32_t line) { return sc.d_verify + kVaccStride + line * kVaccSetWords; }
+
 int ensure_verify(Scratch& sc) {
   if (sc.d_verify) return KVSEP_OK;
-  std::vector<unsigned long long> init(kVaccStride * (2 + kVaccShards), 0ull);
-  init[0] = ~0ull;            // default first_bad
-  init[kVaccStride] = ~0ull;  // vacc[0]
+  std::vector<unsigned long long> init(kVaccStride + kVaccLines * kVaccSetWords, 0ull);
+  init[0] = ~0ull;  // default first_bad
+  for (uint32_t l = 0; l < kVaccLines; ++l) init[kVaccStride + l * kVaccSetWords] = ~0ull;  // each set's vacc[0]
   KVSEP_HIP(hipMalloc(&sc.d_verify, init.size() * 8));
   KVSEP_HIP(hipMemcpy(sc.d_verify, init.data(), init.size() * 8, hipMemcpyHostToDevice));
+  sc.vacc_dirty = 0;
+  return KVSEP_OK;
+}
+
+// Puts accumulator set `line` back in its reset state, in stream order (capturable: two memsets).  Needed after a call
+// that failed once its CRC kernel was enqueued: the kernel's posts stay in the set, and with no publishing kernel after
+// them nothing resets it -- the next verdict would inherit a stale count and first_bad.
+int reset_vacc(Scratch& sc, uint32_t line, hipStream_t s) {
+  unsigned long long* v = vacc_set(sc, line);
+  KVSEP_HIP(hipMemsetAsync(v, 0, kVaccSetWords * 8, s));
+  KVSEP_HIP(hipMemsetAsync(v, 0xff, 8, s));
+  sc.vacc_dirty &= ~(1u << line);
   return KVSEP_OK;
 }
 
@@ -2047,9 +2067,10 @@ void launch_pieces(bool planned, bool dyn, bool verify, int variant, unsigned gr
   else launch_pieces_vv<false>(planned, dyn, variant, grid, s, a);
 }
 
-int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* base, const uint64_t* off,
-                    const uint64_t* len, const uint32_t* init, const uint32_t* expect, uint32_t* out,
-                    uint64_t* first_bad, uint64_t* nbad, uint64_t count, uint64_t total_bytes, uint64_t max_len);
+int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, bool capturing, const void* base,
+                    const uint64_t* off, const uint64_t* len, const uint32_t* init, const uint32_t* expect,
+                    uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count, uint64_t total_bytes,
+                    uint64_t max_len);
 
 // Every use of a Scratch is bracketed by acquire/release (event ordering across streams).
 int launch_batch(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* base, const uint64_t* off,
@@ -2069,16 +2090,47 @@ int launch_batch(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* ba
   const bool capturing = cap != hipStreamCaptureStatusNone;
   int rc = capturing ? KVSEP_OK : acquire(sc, s);
   if (rc) return rc;
-  rc = launch_batch_in(c, sc, s, base, off, len, init, expect, out, first_bad, nbad, count, total_bytes, max_len);
-  if (rc) return rc;
+  rc = launch_batch_in(c, sc, s, capturing, base, off, len, init, expect, out, first_bad, nbad, count, total_bytes,
+                       max_len);
+  if (rc) {
+    if (!capturing) (void)release(sc, s);  // whatever was enqueued stays ordered before the scratch's next user
+    return rc;
+  }
   return capturing ? KVSEP_OK : release(sc, s);
 }
 
-int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* base, const uint64_t* off,
-                    const uint64_t* len, const uint32_t* init, const uint32_t* expect, uint32_t* out,
-                    uint64_t* first_bad, uint64_t* nbad, uint64_t count, uint64_t total_bytes, uint64_t max_len) {
-  const bool planned = !(max_len != 0 && max_len <= c->piece_bytes);
+int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, PiecesArgs& a, const void* base,
+                      const uint64_t* off, const uint64_t* len, const uint32_t* init, const uint32_t* expect,
+                      uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count, uint64_t total_bytes,
+                      uint64_t max_len);
+
+int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, bool capturing, const void* base,
+                    const uint64_t* off, const uint64_t* len, const uint32_t* init, const uint32_t* expect,
+                    uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count, uint64_t total_bytes,
+                    uint64_t max_len) {
   PiecesArgs a{};
+  uint32_t line = 0;
+  if (expect) {
+    int rc = ensure_verify(sc);
+    if (rc) return rc;
+    line = capturing ? 1 + (sc.vacc_next++ % (kVaccLines - 1)) : 0;
+    if (sc.vacc_dirty & (1u << line)) {
+      rc = reset_vacc(sc, line, s);
+      if (rc) return rc;
+    }
+    a.vacc = vacc_set(sc, line);  // the accumulators, in their reset state: the kernels publish the verdict
+  }
+  const int rc = launch_batch_body(c, sc, s, a, base, off, len, init, expect, out, first_bad, nbad, count, total_bytes,
+                                   max_len);
+  if (rc && expect) sc.vacc_dirty |= 1u << line;  // a kernel may have posted to the set: reset it before its next use
+  return rc;
+}
+
+int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, PiecesArgs& a, const void* base,
+                      const uint64_t* off, const uint64_t* len, const uint32_t* init, const uint32_t* expect,
+                      uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count, uint64_t total_bytes,
+                      uint64_t max_len) {
+  const bool planned = !(max_len != 0 && max_len <= c->piece_bytes);
   a.base = static_cast<const uint8_t*>(base);
   a.off = off;
   a.len = len;
@@ -2088,13 +2140,10 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
   a.piece_bytes = planned ? piece_for(c, total_bytes, &a.zpiece) : c->piece_bytes;
   a.tabs = c->d_tabs;
   if (expect) {
-    int rc = ensure_verify(sc);
-    if (rc) return rc;
     if (!first_bad || !nbad) {
       first_bad = reinterpret_cast<uint64_t*>(sc.d_verify);
       nbad = reinterpret_cast<uint64_t*>(sc.d_verify + 1);
     }
-    a.vacc = sc.d_verify + kVaccStride;  // the accumulators, in their reset state: the kernels publish the verdict
     if (count == 0) {          // nothing to check, no kernel: the verdict is "none" (first_bad = ~0, nbad = 0)
       KVSEP_HIP(hipMemsetAsync(first_bad, 0xff, 8, s));
       KVSEP_HIP(hipMemsetAsync(nbad, 0, 8, s));
@@ -2179,6 +2228,10 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void*
     launch_pieces(planned, dyn, expect != nullptr, c->variant, grid, s, a);
   }
   KVSEP_HIP(hipGetLastError());
+  if (c->inject_failure) {  // fault injection (tests): fail between the CRC kernel and the combine kernel
+    c->inject_failure = false;
+    return set_err(KVSEP_EHIP, "injected failure after the CRC kernel (kvsep_crc32c_ctx_inject_failure)");
+  }
   if (c->timing && e0 && e1) {
     KVSEP_HIP(hipEventRecord(e1, s));
     c->ev_pending.emplace_back(e0, e1);
@@ -2217,6 +2270,7 @@ void free_scratch(Scratch& sc) {
 HostStaging& ctx_staging(kvsep_crc32c_ctx* c) { return c->staging; }
 std::mutex& ctx_mutex(kvsep_crc32c_ctx* c) { return c->mu; }
 int ctx_device(kvsep_crc32c_ctx* c) { return c->device; }
+int ctx_host_node(kvsep_crc32c_ctx* c) { return c->host_node; }
 uint64_t ctx_piece_bytes(kvsep_crc32c_ctx* c) { return c->piece_bytes; }
 void set_last_error(const char* msg) { g_last_error = msg; }
 }  // namespace kvsep
@@ -2246,6 +2300,7 @@ int kvsep_crc32c_ctx_create(int device, kvsep_crc32c_ctx** out) {
   auto* c = new kvsep_crc32c_ctx();
   c->device = device;
   c->num_cus = prop.multiProcessorCount;
+  c->host_node = kvsep_device_numa_node(device);
   diag_env(c);  // tools build only: no environment variable reaches the shipped library's kernel choice
   int rc = upload_tables(c);
   if (rc) {
@@ -2293,6 +2348,20 @@ int kvsep_crc32c_ctx_set_kernel(kvsep_crc32c_ctx* c, int kernel) {
   if (!c || kernel < 0 || kernel > 7) return set_err(KVSEP_EINVAL, "kernel must be 0..7");
   std::lock_guard<std::mutex> g(c->mu);
   c->kernel = kernel;
+  return KVSEP_OK;
+}
+
+int kvsep_crc32c_ctx_set_host_node(kvsep_crc32c_ctx* c, int node) {
+  if (!c || node < -1) return set_err(KVSEP_EINVAL, "node must be >= -1");
+  std::lock_guard<std::mutex> g(c->mu);
+  c->host_node = node;
+  return KVSEP_OK;
+}
+
+int kvsep_crc32c_ctx_inject_failure(kvsep_crc32c_ctx* c) {
+  if (!c) return set_err(KVSEP_EINVAL, "null ctx");
+  std::lock_guard<std::mutex> g(c->mu);
+  c->inject_failure = true;
   return KVSEP_OK;
 }
 
@@ -2415,9 +2484,12 @@ int kvsep_sst_verify_device(kvsep_crc32c_ctx* c, void* stream, const void* file_
                                                                         len, sc.d_sst_len1, sc.d_sst_stored, count);
     KVSEP_HIP(hipGetLastError());
   }
-  rc = launch_batch_in(c, sc, s, file_base, off, sc.d_sst_len1, nullptr, sc.d_sst_stored, out, first_bad, nbad, count,
-                       total_bytes + count, max_len ? max_len + 1 : 0);
-  if (rc) return rc;
+  rc = launch_batch_in(c, sc, s, capturing, file_base, off, sc.d_sst_len1, nullptr, sc.d_sst_stored, out, first_bad,
+                       nbad, count, total_bytes + count, max_len ? max_len + 1 : 0);
+  if (rc) {
+    if (!capturing) (void)release(sc, s);
+    return rc;
+  }
   return capturing ? KVSEP_OK : release(sc, s);
 }
 

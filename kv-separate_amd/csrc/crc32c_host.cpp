@@ -1,12 +1,11 @@
 // crc32c_host.cpp -- host half of libkvsep_crc32c: the scalar drop-in (Extend / Value / Mask /
-// Unmask / AcceleratedCRC32C), the host-memory batch entry points (pinned staging, H2D, kernel,
-// D2H over two streams), and build info.
+// Unmask / AcceleratedCRC32C; its host legs are in host_crc.cpp), the host-memory batch entry points (pinned staging,
+// H2D, kernel, D2H over two streams), and build info.
 //
 // Reference interfaces replaced (see include/kvsep_crc32c.h for the full list):
 //   util/crc32c.h:17   leveldb::crc32c::Extend      -> kvsep_crc32c_extend
 //   port/port_stdcxx.h:142 port::AcceleratedCRC32C  -> kvsep_accelerated_crc32c
 #include <hip/hip_runtime.h>
-#include <immintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -23,17 +22,18 @@
 #include <string>
 
 #include "../../include/kvsep_crc32c.h"
-#include "gf2.h"
+#include "host_crc.h"
 #include "kvsep_internal.h"
+#include "numa.h"
 
 namespace kvsep {
 
-CopyPool* copy_pool_create() {
+CopyPool* copy_pool_create(const std::vector<int>& cpus) {
   int n = 7;  // + the caller: 8 copiers
   if (const char* v = std::getenv("KVSEP_COPY_THREADS")) n = std::max(0, std::atoi(v) - 1);
-  const int hw = int(std::thread::hardware_concurrency());
+  const int hw = cpus.empty() ? int(std::thread::hardware_concurrency()) : int(cpus.size());
   if (hw > 0) n = std::min(n, std::max(0, hw - 1));
-  return new CopyPool(n);
+  return new CopyPool(n, cpus);
 }
 void copy_pool_destroy(CopyPool* p) { delete p; }
 void copy_pool_run(CopyPool* p, const CopySeg* segs, uint64_t nseg) { p->run(segs, nseg); }
@@ -55,200 +55,6 @@ namespace {
 
 std::atomic<uint64_t> g_offload_threshold{64ull << 20};
 std::atomic<uint64_t> g_gpu_calls{0}, g_host_calls{0}, g_gpu_failures{0};
-
-// ------------------------------------------------------------------ host CRC (SSE4.2)
-// The crc32 instruction implements exactly the reflected Castagnoli register update of
-// util/crc32c.cc:287-292 without the ~0 conditioning, so Extend = ~crc32(~init, data).
-// Three independent streams hide the instruction's 3-cycle latency; they are merged with
-// the zero-byte shift R(A||B) = Z_|B|(R(A)) ^ R(B), Z_L from four byte tables per lane length L.  Lane lengths 4 KiB,
-// 1 KiB and 256 B, largest first, so a 4 KiB SST block (the reference's commonest Extend) runs 3-way too: 3 x 1 KiB,
-// 3 x 256 B, then 256 B serially.
-struct ShiftTables {
-  uint32_t t[4][256];
-};
-
-constexpr uint64_t kLaneBlocks[3] = {4096, 1024, 256};  // bytes per stream per round of the 3-way loop
-const ShiftTables* shift_tables() {
-  // generated by GF(2) matrix squaring (gf2.h, the same generator as the device tables): microseconds, where stepping
-  // every table entry over L zero bytes cost ~40 ms on the first Extend that reached the 3-way loop
-  static const std::vector<ShiftTables> tabs = [] {
-    std::vector<ShiftTables> v(3);
-    for (int s = 0; s < 3; ++s) gf2::byte_tables(gf2::zero_bytes_map(kLaneBlocks[s]), &v[s].t[0][0]);
-    return v;
-  }();
-  return tabs.data();
-}
-
-inline uint32_t shift_lane(const ShiftTables& s, uint32_t v) {
-  return s.t[0][v & 0xffu] ^ s.t[1][(v >> 8) & 0xffu] ^ s.t[2][(v >> 16) & 0xffu] ^ s.t[3][v >> 24];
-}
-
-// ------------------------------------------------------------------ host CRC (VPCLMULQDQ folding)
-// CPUs with AVX-512 carry-less multiply (the MI355X hosts' EPYC 9005 / Zen 5 among them) fold instead: four 512-bit
-// accumulators, each holding four 16-B lanes of the stream, are carried 256 B forward per round with two carry-less
-// products per lane and XORed into the next 256 B; at the end the 16 lanes are folded into one 16-B value X (taking in
-// the remainder's whole 64-B and 16-B chunks on the way), and the register after the folded bytes is
-// crc32(crc32(0, X.lo), X.hi) -- X is congruent, mod P, to everything folded into it, placed at the last 16 bytes.
-// The initial register is XORed into the first four bytes (gf2.h: a register before bytes q..q+3 is interchangeable
-// with a word XORed into them).
-//
-// Constants.  A lane loaded little-endian has stream bit j at integer bit j, the coefficient of x^(127-j) relative to
-// the lane's end; its low qword is the high-degree half: A = x^64 Lo + Hi.  A carry-less product of two 64-bit
-// reflected values (bit i = x^(63-i)) read as a 128-bit lane is their product times x.  Carrying A forward by 8D
-// bits (D bytes) therefore takes clmul(Lo, K_lo) ^ clmul(Hi, K_hi) with K_lo = x^(8D+63) mod P and
-// K_hi = x^(8D-1) mod P, each a 32-bit reflected residue placed in the qword's upper half (x^d at bit 63-d).
-struct FoldConsts {
-  uint64_t k256[2], k64[2], k48[2], k32[2], k16[2];  // {K_lo, K_hi} for D = 256, 64, 48, 32, 16 bytes
-};
-
-uint32_t xpow_mod(uint64_t e) {  // x^e mod P, reflected 32-bit form (bit 31 = x^0)
-  uint32_t sq[64];
-  gf2::x2n_table(sq);
-  uint32_t r = 0x80000000u;
-  for (int k = 0; e; ++k, e >>= 1)
-    if (e & 1u) r = gf2::mulmod(r, sq[k]);
-  return r;
-}
-
-const FoldConsts& fold_consts() {
-  static const FoldConsts fc = [] {
-    FoldConsts f;
-    auto set = [](uint64_t* k, uint64_t d) {
-      k[0] = uint64_t(xpow_mod(8 * d + 63)) << 32;
-      k[1] = uint64_t(xpow_mod(8 * d - 1)) << 32;
-    };
-    set(f.k256, 256);
-    set(f.k64, 64);
-    set(f.k48, 48);
-    set(f.k32, 32);
-    set(f.k16, 16);
-    return f;
-  }();
-  return fc;
-}
-
-// The folding path needs AVX-512F and VPCLMULQDQ (checked once; KVSEP_HOST_CRC=sse42 keeps the crc32 path, for A/B).
-bool fold_available() {
-  static const bool ok = [] {
-    const char* e = std::getenv("KVSEP_HOST_CRC");
-    if (e && std::strcmp(e, "sse42") == 0) return false;
-#ifdef __HIP_DEVICE_COMPILE__  // this file is compiled as HIP: the gfx950 pass parses host code but has no CPU builtins
-    return false;
-#else
-    __builtin_cpu_init();
-    return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("vpclmulqdq") &&
-           __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.2");
-#endif
-  }();
-  return ok;
-}
-
-constexpr size_t kFoldMin = 128;  // below, the crc32 loop is as fast (64-96 B: 10-14 ns a call either way)
-
-#define KVSEP_FOLD_TARGET __attribute__((target("avx512f,vpclmulqdq,pclmul,sse4.2")))
-// x carried forward by k's distance ({K_lo, K_hi} in every 128-bit lane), XORed into d
-KVSEP_FOLD_TARGET inline __attribute__((always_inline)) __m512i fold(__m512i x, __m512i k, __m512i d) {
-  return _mm512_ternarylogic_epi64(_mm512_clmulepi64_epi128(x, k, 0x00), _mm512_clmulepi64_epi128(x, k, 0x11), d, 0x96);
-}
-KVSEP_FOLD_TARGET inline __attribute__((always_inline)) __m128i fold128(__m128i x, const uint64_t* k) {
-  const __m128i kk = _mm_loadu_si128(reinterpret_cast<const __m128i*>(k));
-  return _mm_xor_si128(_mm_clmulepi64_si128(x, kk, 0x00), _mm_clmulepi64_si128(x, kk, 0x11));
-}
-
-// Folds whole 256-B rounds (n >= 256), then the remainder's whole 64-B and 16-B chunks (n >= kFoldMin), starting from
-// register l; advances p / n past them (n < 16 is left for the crc32 tail) and returns the register after them.
-KVSEP_FOLD_TARGET uint32_t fold_bulk(uint32_t l, const uint8_t*& p, size_t& n) {
-  const FoldConsts& fc = fold_consts();
-  const __m512i k64 = _mm512_broadcast_i32x4(_mm_loadu_si128(reinterpret_cast<const __m128i*>(fc.k64)));
-  const __m512i init = _mm512_zextsi128_si512(_mm_cvtsi32_si128(int(l)));
-  __m512i x3;
-  if (n >= 256) {  // four accumulators, 256-B rounds
-    const __m512i k256 = _mm512_broadcast_i32x4(_mm_loadu_si128(reinterpret_cast<const __m128i*>(fc.k256)));
-    __m512i x0 = _mm512_xor_si512(_mm512_loadu_si512(p), init), x1 = _mm512_loadu_si512(p + 64),
-            x2 = _mm512_loadu_si512(p + 128);
-    x3 = _mm512_loadu_si512(p + 192);
-    p += 256;
-    n -= 256;
-    while (n >= 256) {
-      x0 = fold(x0, k256, _mm512_loadu_si512(p));
-      x1 = fold(x1, k256, _mm512_loadu_si512(p + 64));
-      x2 = fold(x2, k256, _mm512_loadu_si512(p + 128));
-      x3 = fold(x3, k256, _mm512_loadu_si512(p + 192));
-      p += 256;
-      n -= 256;
-    }
-    x1 = fold(x0, k64, x1);
-    x2 = fold(x1, k64, x2);
-    x3 = fold(x2, k64, x3);
-  } else {  // kFoldMin <= n < 256: one accumulator from the start
-    x3 = _mm512_xor_si512(_mm512_loadu_si512(p), init);
-    p += 64;
-    n -= 64;
-  }
-  while (n >= 64) {  // the remainder's whole 64-B chunks, one accumulator
-    x3 = fold(x3, k64, _mm512_loadu_si512(p));
-    p += 64;
-    n -= 64;
-  }
-  __m128i r = _mm512_extracti32x4_epi32(x3, 3);
-  r = _mm_xor_si128(r, fold128(_mm512_extracti32x4_epi32(x3, 0), fc.k48));
-  r = _mm_xor_si128(r, fold128(_mm512_extracti32x4_epi32(x3, 1), fc.k32));
-  r = _mm_xor_si128(r, fold128(_mm512_extracti32x4_epi32(x3, 2), fc.k16));
-  while (n >= 16) {  // and its whole 16-B chunks
-    r = _mm_xor_si128(fold128(r, fc.k16), _mm_loadu_si128(reinterpret_cast<const __m128i*>(p)));
-    p += 16;
-    n -= 16;
-  }
-  uint64_t c = _mm_crc32_u64(0, uint64_t(_mm_cvtsi128_si64(r)));
-  c = _mm_crc32_u64(c, uint64_t(_mm_extract_epi64(r, 1)));
-  return uint32_t(c);
-}
-
-__attribute__((target("sse4.2"))) uint32_t host_crc(uint32_t init, const uint8_t* p, size_t n) {
-  uint64_t l = uint32_t(~init);
-  if (n >= kFoldMin && fold_available()) l = fold_bulk(uint32_t(l), p, n);
-  while (n && (reinterpret_cast<uintptr_t>(p) & 7)) {
-    l = _mm_crc32_u8(uint32_t(l), *p++);
-    --n;
-  }
-  if (n >= 3 * kLaneBlocks[2]) {
-    const ShiftTables* st = shift_tables();
-    for (int s = 0; s < 3; ++s) {
-      const uint64_t L = kLaneBlocks[s];
-      while (n >= 3 * L) {
-        uint64_t a = l, b = 0, c = 0;
-        const uint8_t* pa = p;
-        const uint8_t* pb = p + L;
-        const uint8_t* pc = p + 2 * L;
-        for (uint64_t i = 0; i < L; i += 8) {
-          uint64_t wa, wb, wc;
-          std::memcpy(&wa, pa + i, 8);
-          std::memcpy(&wb, pb + i, 8);
-          std::memcpy(&wc, pc + i, 8);
-          a = _mm_crc32_u64(a, wa);
-          b = _mm_crc32_u64(b, wb);
-          c = _mm_crc32_u64(c, wc);
-        }
-        // R(A||B||C) = Z(Z(a) ^ b) ^ c with Z = advance over L zero bytes
-        l = shift_lane(st[s], shift_lane(st[s], uint32_t(a)) ^ uint32_t(b)) ^ uint32_t(c);
-        p += 3 * L;
-        n -= 3 * L;
-      }
-    }
-  }
-  while (n >= 8) {
-    uint64_t w;
-    std::memcpy(&w, p, 8);
-    l = _mm_crc32_u64(l, w);
-    p += 8;
-    n -= 8;
-  }
-  while (n) {
-    l = _mm_crc32_u8(uint32_t(l), *p++);
-    --n;
-  }
-  return ~uint32_t(l);
-}
 
 // ------------------------------------------------------------------ staging pipeline
 constexpr uint64_t kSlotBytes = 64ull << 20;
@@ -301,6 +107,9 @@ int ensure_staging(kvsep_crc32c_ctx* c) {
   }
   DeviceGuard dg(ctx_device(c));
   if (dg.err != hipSuccess) return hip_fail("hipSetDevice", dg.err);
+  // On the device's NUMA node (round 5): this thread while it allocates the pinned slots (its preferred memory node),
+  // then the copier threads that fill them -- the staged bytes never cross the socket link on their way to the GPU.
+  numa::ScopedBind bind(ctx_host_node(c));
   const int rc = ensure_staging_once(s);
   if (rc != KVSEP_OK) {
     std::string msg = kvsep_last_error();
@@ -312,7 +121,8 @@ int ensure_staging(kvsep_crc32c_ctx* c) {
     return rc;
   }
   s.failures = 0;
-  s.pool = copy_pool_create();
+  s.cpus = bind.cpus();
+  s.pool = copy_pool_create(s.cpus);
   s.ready = true;
   return KVSEP_OK;
 }
@@ -642,6 +452,19 @@ int kvsep_crc32c_batch_host_span(kvsep_crc32c_ctx* c, const char* host_base, uin
   return KVSEP_OK;
 }
 
+int kvsep_crc32c_ctx_host_placement(kvsep_crc32c_ctx* c, int* device_node, int* staging_node, int* cpus, int cap) {
+  if (!c) {
+    set_last_error("null ctx");
+    return KVSEP_EINVAL;
+  }
+  std::lock_guard<std::mutex> g(ctx_mutex(c));
+  const HostStaging& s = ctx_staging(c);
+  if (device_node) *device_node = ctx_host_node(c);
+  if (staging_node) *staging_node = s.ready ? numa::page_node(s.h_data[0]) : -1;
+  for (int i = 0; cpus && i < cap && i < int(s.cpus.size()); ++i) cpus[i] = s.cpus[i];
+  return int(s.cpus.size());
+}
+
 int kvsep_crc32c_batch_host(kvsep_crc32c_ctx* c, const uint32_t* init, const char* const* ptr, const uint64_t* len,
                             uint32_t* out, uint64_t count) {
   return kvsep::batch_host_tee(c, init, ptr, len, out, count, nullptr);
@@ -665,7 +488,9 @@ int kvsep_abi_version(void) { return KVSEP_ABI_VERSION; }
 
 const char* kvsep_build_info(void) {
   return "kvsep_crc32c: gfx950 HIP kernels (LDS-replicated Z_1024 stride chains, v_perm addressing), "
-         "host VPCLMULQDQ fold / SSE4.2 crc32 path, ABI 2";
+         "host legs: VPCLMULQDQ fold / SSE4.2 crc32 / portable slicing-by-8, ABI 3";
 }
+
+const char* kvsep_crc32c_host_path(void) { return host_leg_name(host_leg()); }
 
 }  // extern "C"

@@ -18,6 +18,7 @@
 
 #include "../../include/kvsep_crc32c.h"
 #include "kvsep_internal.h"
+#include "numa.h"
 
 struct kvsep_crc32c_group {
   std::vector<int> devices;
@@ -29,19 +30,22 @@ struct kvsep_crc32c_group {
 
 namespace {
 
-// Runs fn(i) for every member i on its own host thread (member 0 on the caller's); first error wins.
+// Runs fn(i) for every member i on its own host thread (member 0 on the caller's), each thread bound for the call to
+// the NUMA node of its member's device (round 5: the staging it fills and the PCIe link it drives are there; the
+// caller's own affinity and memory policy come back when member 0 is done); first error wins.
 template <typename Fn>
-int fan_out(int n, Fn&& fn) {
+int fan_out(kvsep_crc32c_group* g, Fn&& fn) {
+  const int n = int(g->ctx.size());
   std::vector<int> rc(n, KVSEP_OK);
   std::vector<std::string> err(n);
   std::vector<std::thread> th;
-  for (int i = 1; i < n; ++i)
-    th.emplace_back([&, i] {
-      rc[i] = fn(i);
-      if (rc[i]) err[i] = kvsep_last_error();  // the error text is thread-local
-    });
-  rc[0] = fn(0);
-  if (rc[0]) err[0] = kvsep_last_error();
+  auto member = [&](int i) {
+    kvsep::numa::ScopedBind bind(kvsep::ctx_host_node(g->ctx[i]));
+    rc[i] = fn(i);
+    if (rc[i]) err[i] = kvsep_last_error();  // the error text is thread-local
+  };
+  for (int i = 1; i < n; ++i) th.emplace_back(member, i);
+  member(0);
   for (auto& t : th) t.join();
   for (int i = 0; i < n; ++i)
     if (rc[i]) {
@@ -148,7 +152,7 @@ int kvsep_crc32c_group_batch_host_span(kvsep_crc32c_group* g, const char* host_b
   std::vector<uint64_t> bounds(n + 1);
   int rc = kvsep_crc32c_partition(len, count, n, bounds.data());
   if (rc) return rc;
-  return fan_out(n, [&](int i) {
+  return fan_out(g, [&](int i) {
     const uint64_t b0 = bounds[i], b1 = bounds[i + 1];
     if (b0 == b1) return int(KVSEP_OK);
     return kvsep_crc32c_batch_host_span(g->ctx[i], host_base, span_bytes, off + b0, len + b0, init ? init + b0 : nullptr,
@@ -220,7 +224,7 @@ int kvsep_crc32c_group_verify_device(kvsep_crc32c_group* g, const void* const* b
   std::lock_guard<std::mutex> lk(g->mu);
   const int n = int(g->ctx.size());
   std::vector<uint64_t> fb(n, UINT64_MAX), nb(n, 0);
-  const int rc = fan_out(n, [&](int i) {
+  const int rc = fan_out(g, [&](int i) {
     if (!count[i]) return int(KVSEP_OK);
     kvsep::DeviceGuard dg(g->devices[i]);
     if (dg.err != hipSuccess) {

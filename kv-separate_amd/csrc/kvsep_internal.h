@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <mutex>
+#include <vector>
 
 #include "copy_pool.h"
 
@@ -25,7 +26,9 @@ struct Scratch {
   void* d_scan_tmp = nullptr;
   size_t scan_tmp_bytes = 0;
   uint32_t* d_counter = nullptr;
-  unsigned long long* d_verify = nullptr;  // [first_bad, nbad] when the caller passes none
+  unsigned long long* d_verify = nullptr;  // [first_bad, nbad] when the caller passes none, then the accumulator sets
+  uint32_t vacc_next = 0;                   // captured verify calls take accumulator sets 1..7 in turn
+  uint32_t vacc_dirty = 0;                  // sets a failed call may have posted to: reset before their next use
   uint64_t* d_sst_len1 = nullptr;           // SST verify: len + 1 ...
   uint32_t* d_sst_stored = nullptr;         // ... and the stored trailer words
   uint64_t cap_sst = 0;
@@ -35,8 +38,8 @@ struct Scratch {
 };
 void free_scratch(Scratch& sc);
 
-// The persistent host copiers of the staging pipeline (copy_pool.h).
-CopyPool* copy_pool_create();
+// The persistent host copiers of the staging pipeline (copy_pool.h), bound to `cpus` when it is not empty.
+CopyPool* copy_pool_create(const std::vector<int>& cpus);
 void copy_pool_destroy(CopyPool* p);
 void copy_pool_run(CopyPool* p, const CopySeg* segs, uint64_t nseg);  // returns when every byte is copied
 
@@ -57,6 +60,7 @@ struct HostStaging {
   hipEvent_t done[kSlots] = {nullptr, nullptr};
   Scratch scratch[kSlots];
   CopyPool* pool = nullptr;
+  std::vector<int> cpus;     // the CPUs the copiers (and the staging allocation) were bound to: the device's NUMA node
   bool ready = false;
   // allocation failed: retried only after a backoff (ensure_staging), so a transient failure is not permanent and
   // a persistent one does not cost an allocation attempt per call
@@ -97,6 +101,7 @@ int batch_host_tee(kvsep_crc32c_ctx* c, const uint32_t* init, const char* const*
 HostStaging& ctx_staging(kvsep_crc32c_ctx* c);
 std::mutex& ctx_mutex(kvsep_crc32c_ctx* c);
 int ctx_device(kvsep_crc32c_ctx* c);
+int ctx_host_node(kvsep_crc32c_ctx* c);  // NUMA node of the device (-1: unknown or binding off)
 uint64_t ctx_piece_bytes(kvsep_crc32c_ctx* c);
 void set_last_error(const char* msg);
 

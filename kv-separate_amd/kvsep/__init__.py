@@ -54,6 +54,17 @@ _SIGS = {
     "kvsep_offload_stats": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "kvsep_crc32c_kernel_name": (ctypes.c_char_p, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]),
     "kvsep_crc32c_extend_host": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
+    "kvsep_crc32c_host_path": (ctypes.c_char_p, []),
+    "kvsep_crc32c_ctx_set_host_node": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "kvsep_crc32c_ctx_host_placement": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                       ctypes.c_void_p, ctypes.c_int]),
+    "kvsep_crc32c_ctx_inject_failure": (ctypes.c_int, [ctypes.c_void_p]),
+    "kvsep_device_pci_bus_id": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
+    "kvsep_pci_numa_node": (ctypes.c_int, [ctypes.c_char_p]),
+    "kvsep_device_numa_node": (ctypes.c_int, [ctypes.c_int]),
+    "kvsep_numa_node_cpus": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
+    "kvsep_bind_process_numa": (ctypes.c_int, [ctypes.c_int]),
+    "kvsep_host_page_node": (ctypes.c_int, [ctypes.c_void_p]),
     "kvsep_crc32c_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "kvsep_crc32c_ctx_destroy": (None, [ctypes.c_void_p]),
     "kvsep_crc32c_ctx_set_piece_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
@@ -205,6 +216,11 @@ def extend_host(init_crc: int, data, n: int | None = None) -> int:
     return lib().kvsep_crc32c_extend_host(init_crc & 0xFFFFFFFF, p, n)
 
 
+def host_path() -> str:
+    """The host leg this process runs ("fold", "sse42" or "portable"; kvsep_crc32c_host_path)."""
+    return lib().kvsep_crc32c_host_path().decode()
+
+
 # ------------------------------------------------------------------ device context
 def _stream_handle(stream):
     if stream is None:
@@ -268,6 +284,23 @@ class Context:
         "sorted" its sorted-window form for ragged batches, "claim" / "claim16" its workgroup-run form with LDS claims,
         8 / 16 lanes per block).  Never changes a result."""
         _check(lib().kvsep_crc32c_ctx_set_kernel(self._h, self.KERNELS[kernel]), "set_kernel")
+
+    def set_host_node(self, node: int):
+        """NUMA node for this context's pinned staging and copier threads (-1: no placement; default: the device's)."""
+        _check(lib().kvsep_crc32c_ctx_set_host_node(self._h, node), "set_host_node")
+
+    def host_placement(self):
+        """-> {"device_node", "staging_node", "copier_cpus"} (kvsep_crc32c_ctx_host_placement)."""
+        dn, sn = ctypes.c_int(), ctypes.c_int()
+        cpus = (ctypes.c_int * 4096)()
+        n = lib().kvsep_crc32c_ctx_host_placement(self._h, ctypes.byref(dn), ctypes.byref(sn), cpus, 4096)
+        if n < 0:
+            _check(n, "host_placement")
+        return {"device_node": dn.value, "staging_node": sn.value, "copier_cpus": list(cpus[:min(n, 4096)])}
+
+    def inject_failure(self):
+        """Fault injection (tests): the next batched call fails right after enqueuing its CRC kernel."""
+        _check(lib().kvsep_crc32c_ctx_inject_failure(self._h), "inject_failure")
 
     def reserve(self, count: int, total_bytes: int):
         _check(lib().kvsep_crc32c_reserve(self._h, count, total_bytes), "reserve")
@@ -632,6 +665,54 @@ def splitmix64_bytes(nbytes: int, seed: int, stream_offset: int = 0) -> np.ndarr
 
 def device_count() -> int:
     return lib().kvsep_device_count()
+
+
+# ------------------------------------------------------------------ topology and host placement
+def pci_bus_id(device: int) -> str:
+    """PCI bus ID of a device, as sysfs spells it ("0000:75:00.0"; kvsep_device_pci_bus_id)."""
+    buf = ctypes.create_string_buffer(64)
+    _check(lib().kvsep_device_pci_bus_id(device, buf, 64), "kvsep_device_pci_bus_id")
+    return buf.value.decode()
+
+
+def pci_numa_node(bus_id: str) -> int:
+    """NUMA node of a PCI function from sysfs (-1 unknown); no device needed."""
+    return lib().kvsep_pci_numa_node(bus_id.encode())
+
+
+def device_numa_node(device: int) -> int:
+    return lib().kvsep_device_numa_node(device)
+
+
+def numa_node_cpus(node: int) -> list:
+    n = lib().kvsep_numa_node_cpus(node, None, 0)
+    cpus = (ctypes.c_int * max(n, 1))()
+    lib().kvsep_numa_node_cpus(node, cpus, n)
+    return list(cpus[:n])
+
+
+def bind_process_numa(node: int) -> int:
+    """Every thread of this process onto the CPUs of `node` it may use, `node` the calling thread's preferred memory
+    node (kvsep_bind_process_numa) -> number of CPUs bound to (0: nothing changed)."""
+    return lib().kvsep_bind_process_numa(node)
+
+
+def host_page_node(addr: int) -> int:
+    """NUMA node of the page at host address `addr` (-1 unknown)."""
+    return lib().kvsep_host_page_node(ctypes.c_void_p(addr))
+
+
+def format_cpulist(cpus) -> str:
+    """[0, 1, 2, 3, 8] -> "0-3,8" (the sysfs cpulist spelling)."""
+    cpus = sorted(set(int(c) for c in cpus))
+    out, i = [], 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(str(cpus[i]) if j == i else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(out)
 
 
 def build_info() -> str:

@@ -104,3 +104,55 @@ def sum_over_ranks(value: float, dist, device) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def gather_objects(obj, dist) -> list:
+    """All-gather one picklable object per rank (the per-rank records of a bench line) -> the list in rank order on
+    every rank; [obj] with no process group.  Over RCCL (the nccl backend) the pickled bytes travel as a device
+    tensor, over gloo on the host."""
+    if not _active(dist):
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def _spread(vals):
+    vals = [v for v in vals if v is not None]
+    if not vals:
+        return None, None, None
+    lo, hi = min(vals), max(vals)
+    return lo, hi, ((hi - lo) / hi if hi else 0.0)
+
+
+def rank_summary(records: list, same_device: bool = False) -> dict:
+    """What a multi-GPU line needs to diagnose itself from its per-rank records (bench.py `per_rank`): whether every
+    rank ran on its own physical GPU (distinct PCI bus IDs; a same-device rehearsal says so instead), the spread of
+    the ranks' own rates and kernel times (skew = (max - min) / max), how far apart they started and finished (wall
+    clock, one host), and the slowest rank."""
+    ids = [r.get("pci_bus_id") for r in records]
+    distinct = all(ids) and len(set(ids)) == len(ids)
+    g_lo, g_hi, g_skew = _spread([r.get("GiBps") for r in records])
+    k_lo, k_hi, k_skew = _spread([r.get("kernel_avg_ms") for r in records])
+    starts = [r["t_start"] for r in records if r.get("t_start") is not None]
+    ends = [r["t_end"] for r in records if r.get("t_end") is not None]
+    rated = [r for r in records if r.get("GiBps") is not None]
+    out = {
+        "ranks": len(records),
+        "distinct_devices": bool(distinct),
+        "same_device_rehearsal": bool(same_device),
+        "pci_bus_ids": sorted(set(i for i in ids if i)),
+        "numa_nodes": sorted(set(r.get("numa_node") for r in records if r.get("numa_node") is not None)),
+        "GiBps_min": g_lo, "GiBps_max": g_hi, "GiBps_skew": g_skew,
+        "kernel_avg_ms_min": k_lo, "kernel_avg_ms_max": k_hi, "kernel_skew": k_skew,
+        "start_skew_ms": (max(starts) - min(starts)) * 1e3 if starts else None,
+        "end_skew_ms": (max(ends) - min(ends)) * 1e3 if ends else None,
+        "slowest_rank": min(rated, key=lambda r: r["GiBps"])["rank"] if rated else None,
+    }
+    for k in ("GiBps_min", "GiBps_max", "kernel_avg_ms_min", "kernel_avg_ms_max"):
+        if out[k] is not None:
+            out[k] = round(out[k], 4)
+    for k in ("GiBps_skew", "kernel_skew", "start_skew_ms", "end_skew_ms"):
+        if out[k] is not None:
+            out[k] = round(out[k], 5)
+    return out

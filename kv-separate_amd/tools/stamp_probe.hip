@@ -8,6 +8,8 @@
 #define KVSEP_STAMPS 1
 #include "../csrc/crc32c_device.hip"
 #include "../csrc/crc32c_host.cpp"
+#include "../csrc/host_crc.cpp"
+#include "../csrc/topology.cpp"
 
 #include <algorithm>
 #include <vector>

@@ -46,18 +46,18 @@ def test_engine_library_does_not_export_the_leveldb_symbol():
 
 
 def test_abi_version():
-    assert kvsep.lib().kvsep_abi_version() == 2
-    assert "ABI 2" in kvsep.build_info()
+    assert kvsep.lib().kvsep_abi_version() == 3
+    assert "ABI 3" in kvsep.build_info()
 
 
 def test_no_environment_variable_reaches_the_kernel_choice():
     """The shipped library reads no variant / kernel-routing variable (those exist only in the KVSEP_DIAG tools
-    build): only KVSEP_STRICT_GPU, KVSEP_COPY_THREADS and KVSEP_HOST_CRC (=sse42: the host leg's crc32 loop instead of
-    the VPCLMULQDQ fold, for A/B), none of which can change a CRC."""
+    build): only KVSEP_STRICT_GPU, KVSEP_COPY_THREADS, KVSEP_HOST_CRC (=sse42 / =portable: a slower host leg, for
+    A/B) and KVSEP_SYSFS_ROOT (where the topology is read: tests fake it), none of which can change a CRC."""
     import re
     strings = open(kvsep.LIB_PATH, "rb").read()
     names = set(re.findall(rb"KVSEP_[A-Z_]{3,}", strings))
-    assert names <= {b"KVSEP_STRICT_GPU", b"KVSEP_COPY_THREADS", b"KVSEP_HOST_CRC"}, names
+    assert names <= {b"KVSEP_STRICT_GPU", b"KVSEP_COPY_THREADS", b"KVSEP_HOST_CRC", b"KVSEP_SYSFS_ROOT"}, names
 
 
 def test_python_extend_rejects_n_past_buffer():
@@ -164,7 +164,18 @@ def test_host_extend_fold_boundaries(oracle):
     remainder's 64-B and 16-B chunks, and leaves < 16 B to the crc32 loop: every length around 256 k for k = 1..9 at
     64 start offsets (the zmm loads' alignments), and every length 0..1023 (both entries, every remainder) at 8
     offsets, three inits each,
-    against the oracle.  On a CPU without AVX-512 VPCLMULQDQ this runs the crc32 path (exact either way)."""
+    against the oracle.  On a CPU without AVX-512 VPCLMULQDQ the fold cannot run: the test then says which leg it
+    checked instead of passing silently on it."""
+    flags = set()
+    for line in open("/proc/cpuinfo"):
+        if line.startswith("flags"):
+            flags = set(line.split(":", 1)[1].split())
+            break
+    leg = kvsep.host_path()
+    if {"avx512f", "vpclmulqdq", "pclmulqdq", "sse4_2"} <= flags and os.environ.get("KVSEP_HOST_CRC") is None:
+        assert leg == "fold", leg
+    elif os.environ.get("KVSEP_HOST_CRC") is None:
+        pytest.skip(f"no AVX-512 VPCLMULQDQ on this CPU: the fold leg cannot run (host leg here: {leg})")
     data = splitmix64_bytes(8192, 91, 0)
     f = kvsep.lib().kvsep_crc32c_extend_host
     lens = sorted({n for k in range(1, 10) for n in range(256 * k - 5, 256 * k + 21)} | {4096, 4097, 4095})

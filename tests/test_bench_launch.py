@@ -29,6 +29,13 @@ def test_gpus_n_launches_n_ranks(n):
     line = json.loads(lines[0])
     assert line["n_gpus"] == n and line["world_size"] == n
     assert line["backend"] == ("gloo" if n > 1 else None)
+    # every rank's record reaches rank 0 through the process group (gloo here, RCCL on the GPUs)
+    pr = line["per_rank"]
+    assert [r["rank"] for r in pr] == list(range(n)) and len({r["pid"] for r in pr}) == n, pr
+    assert all(r["cpu_affinity"] and r["GiBps"] == 1.0 for r in pr), pr
+    sm = line["per_rank_summary"]
+    assert sm["ranks"] == n and sm["start_skew_ms"] is not None and sm["GiBps_skew"] == 0.0, sm
+    assert sm["distinct_devices"] is False and sm["same_device_rehearsal"] is False  # no device: not distinct
 
 
 def test_world_size_mismatch_is_refused():

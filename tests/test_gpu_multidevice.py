@@ -280,3 +280,11 @@ def test_bench_self_launch_eight_ranks_config2_every_block():
     p = line["parity"]
     assert p["blocks_checked_vs_reference"] == 524288 and p["blocks_sampled_vs_oracle"] == 0, p
     assert p["every_block_checked"] and p["mismatches"] == 0, p
+    # eight per-rank records; all eight ran on the one GPU here, and the line says so
+    pr = line["per_rank"]
+    assert [r["rank"] for r in pr] == list(range(8)) and len({r["pid"] for r in pr}) == 8, pr
+    assert len({r["pci_bus_id"] for r in pr}) == 1 and pr[0]["pci_bus_id"], pr
+    assert all(r["kernel_avg_ms"] > 0 and r["GiBps"] > 0 and r["elapsed_s"] > 0 for r in pr), pr
+    sm = line["per_rank_summary"]
+    assert sm["ranks"] == 8 and sm["same_device_rehearsal"] and not sm["distinct_devices"], sm
+    assert sm["GiBps_min"] <= sm["GiBps_max"] and 0 <= sm["GiBps_skew"] < 1 and sm["slowest_rank"] in range(8), sm

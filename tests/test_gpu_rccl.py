@@ -87,3 +87,15 @@ def test_bench_torchrun_one_rank_rccl():
     p = line["parity"]
     assert p["every_block_checked"] and p["blocks_checked_vs_reference"] == 65536 and p["mismatches"] == 0, p
     assert line["host_roundtrip_parity"] is True and line["host_roundtrip_GiBps"] > 0, line
+    # the rank's own record, gathered over RCCL, names the physical GPU and where its host legs ran
+    import re
+    pr = line["per_rank"]
+    assert len(pr) == 1 and pr[0]["rank"] == 0 and pr[0]["local_rank"] == 0, pr
+    bdf = pr[0]["pci_bus_id"]
+    assert re.fullmatch(r"[0-9a-f]{4}:[0-9a-f]{2}:[0-9a-f]{2}\.[0-7]", bdf or ""), pr
+    node_path = f"/sys/bus/pci/devices/{bdf}/numa_node"
+    sys_node = int(open(node_path).read()) if os.path.exists(node_path) else -1
+    assert pr[0]["numa_node"] == sys_node, (pr, sys_node)
+    assert pr[0]["kernel_avg_ms"] > 0 and pr[0]["GiBps"] > 0 and pr[0]["roundtrip_GiBps"] > 0, pr
+    sm = line["per_rank_summary"]
+    assert sm["ranks"] == 1 and sm["distinct_devices"] and sm["pci_bus_ids"] == [bdf], sm
