@@ -267,6 +267,33 @@ __device__ __forceinline__ uint4 mask_low(uint4 c, uint32_t k) {
   return make_uint4(c.x & m(0), c.y & m(1), c.z & m(2), c.w & m(3));
 }
 
+// The steps of the kernel templates below that the KVSEP_DIAG tools build replaces in its A/B forms and ablations
+// (crc32c_diag.inc: other types with these members; the ablations give wrong results by design).  Those types exist only
+// in that build: Exact is the only one the shipped library has, so no kernel it can instantiate computes anything but
+// CRC-32C.
+struct Exact {
+  static constexpr bool kPad = true;        // the wide kernel's padded head (stage<kPad>, round 4)
+  static constexpr bool kHeadTail = true;   // the wide kernel's serial head / tail bytes
+  static constexpr bool kShortcut = false;  // short items run their whole chain (no short_item member needed)
+  static constexpr bool kMerge = true;      // the lane merge (no unmerged member needed)
+  static constexpr int kTreeLevels = 6;     // the wide kernel's lane tree: 64 lanes
+  static constexpr bool kDrain = false;     // the sorted-window kernel drains nothing after a group
+  // one stride-chain step c' = w ^ Z_row(c) through the LDS table: the wide kernel's Z_1024 (fold), the narrow kernels'
+  // layout Lay (nfold)
+  __device__ static __forceinline__ uint32_t fold(const uint8_t* lds, uint32_t c, uint32_t w, uint32_t lc0,
+                                                  uint32_t lc1) {
+    return fold_step(lds, c, w, lc0, lc1);
+  }
+  template <typename Lay>
+  __device__ static __forceinline__ uint32_t nfold(const uint8_t* lds, uint32_t c, uint32_t w, uint32_t lc0,
+                                                   uint32_t lc1) {
+    return Lay::fold(lds, c, w, lc0, lc1);
+  }
+  // the sorted-window kernel's emit / join points (the round-3 bisection's compare variants live in the diag build)
+  __device__ static __forceinline__ void sorted_emit(const PiecesArgs&, uint64_t, uint32_t) {}
+  __device__ static __forceinline__ void sorted_join(const PiecesArgs&, bool, uint64_t, uint32_t, uint32_t, uint32_t) {}
+};
+
 // Raw CRC register after consuming the staged item [ps, pe) from register `reg` (no final inversion).
 // kPad: the padded head of stage<kPad>: `reg` is the register at hbase (rewound), the first chunk's bytes before ps
 // are zeroed here.
@@ -278,20 +305,15 @@ __device__ __forceinline__ uint4 mask_low(uint4 c, uint32_t k) {
 // lets the compiler keep all 16 LDS lookups of a row in flight instead of 2 -- and (b) the next item's
 // loads are the most recent ones, so every wait of this item stays a counted vmcnt that leaves them in
 // flight across the lane merge.
-template <int kG, bool kNT, int kAbl = 0, bool kAlign = false, bool kPad = false,
-          typename Next>  // kAbl != 0: ablations (wrong)
+template <int kG, bool kNT, bool kAlign, bool kPad, typename Ext, typename Next>
 __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, uint32_t reg, uint32_t lane,
                                            uint32_t lc0, uint32_t lc1, Next&& next) {
-  if (kAbl == 7 && s.K <= uint64_t(kG)) {  // ablation: a short item's chain is free (its loads are still used)
-    next();
-    uint32_t x = reg ^ s.v.x ^ s.v.w ^ s.et.x ^ s.tc.y ^ s.hc.z;
-#pragma unroll
-    for (int i = 0; i < kG; ++i) x ^= s.A[i].x ^ s.A[i].y ^ s.A[i].z ^ s.A[i].w;
-    return x;
+  if constexpr (Ext::kShortcut) {
+    if (s.K <= uint64_t(kG)) return Ext::template short_item<kG>(s, reg, next);
   }
   if (s.K) {
     const uint64_t K = s.K, last = K - 1;
-    if (kAbl != 3 && s.ps < s.h0) reg = serial16(lds, reg, uniform4(s.hc), int(s.ps - s.hbase), int(s.h0 - s.hbase));
+    if (Ext::kHeadTail && s.ps < s.h0) reg = serial16(lds, reg, uniform4(s.hc), int(s.ps - s.hbase), int(s.h0 - s.hbase));
     uint4 v = s.v_ok ? s.v : make_uint4(0, 0, 0, 0);
     if (s.seg == s.h0) {  // the head register enters as pending word at h0
       if (kPad) v = mask_low(v, uint32_t(s.ps - s.h0));
@@ -301,14 +323,10 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
 
 #define KVSEP_ROW(V)                                  \
   do {                                                \
-    if (kAbl == 2) {                                  \
-      c0 ^= (V).x; c1 ^= (V).y; c2 ^= (V).z; c3 ^= (V).w; \
-    } else {                                          \
-    c0 = fold_step(lds, c0, (V).x, lc0, lc1);         \
-    c1 = fold_step(lds, c1, (V).y, lc0, lc1);         \
-    c2 = fold_step(lds, c2, (V).z, lc0, lc1);         \
-    c3 = fold_step(lds, c3, (V).w, lc0, lc1);         \
-    }                                                 \
+    c0 = Ext::fold(lds, c0, (V).x, lc0, lc1);         \
+    c1 = Ext::fold(lds, c1, (V).y, lc0, lc1);         \
+    c2 = Ext::fold(lds, c2, (V).z, lc0, lc1);         \
+    c3 = Ext::fold(lds, c3, (V).w, lc0, lc1);         \
   } while (0)
 // The group's loads go out before any of its compute: the scheduler would otherwise sink them below the
 // first row's lookups and shorten the time they are in flight (the loop is HBM-latency bound).
@@ -322,15 +340,6 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     uint64_t r = 1;
     for (; r + 2 * kG <= K; r += kG) {  // full group in A, another full group after it: no next item yet
       uint4 B[kG];
-      if (kAbl == 5) {  // diag variant (exact): fold the group, then load the next one (no rows in flight meanwhile)
-#pragma unroll
-        for (int i = 0; i < kG; ++i) KVSEP_ROW(s.A[i]);
-        __builtin_amdgcn_sched_barrier(0);
-        KVSEP_LOADB(r + kG, false);
-#pragma unroll
-        for (int i = 0; i < kG; ++i) s.A[i] = B[i];
-        continue;
-      }
       KVSEP_LOADB(r + kG, false);  // rows r+kG .. r+2kG-1 <= K-1: no clamp
 #pragma unroll
       for (int i = 0; i < kG; ++i) KVSEP_ROW(s.A[i]);
@@ -354,7 +363,7 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
       if (r + i < K) KVSEP_ROW(s.A[i]);
 #undef KVSEP_LOADB
 #undef KVSEP_ROW
-    if (kAbl == 1) return c0 ^ c1 ^ c2 ^ c3 ^ lane;
+    if constexpr (!Ext::kMerge) return Ext::unmerged(c0, c1, c2, c3, lane);
     // lane merge: pending word at (16*lane + 12) of the last row
     uint32_t p = zmap_x(lds, kZ4Off, c0, c1);
     p = zmap_x(lds, kZ4Off, p, c2);
@@ -366,7 +375,7 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     // The partner of an active lane l is l - 2^j: DPP row_shr for j < 4 (within a 16-lane row), lane
     // reads for j = 4, 5 -- no ds_bpermute round trips on this latency-bound chain.
 #pragma unroll
-    for (int j = 0; j < (kAbl == 4 ? 0 : 6); ++j) {
+    for (int j = 0; j < Ext::kTreeLevels; ++j) {
       uint32_t o;
       if (j == 0) {
         o = row_shr<1>(p);
@@ -390,7 +399,7 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     reg = zmap(lds, kZ4Off, p);                              // register at ar (kAlign) or a1
   } else {
     next();
-    if (kAbl != 3 && s.ps < s.h0) reg = serial16(lds, reg, uniform4(s.hc), int(s.ps - s.hbase), int(s.h0 - s.hbase));
+    if (Ext::kHeadTail && s.ps < s.h0) reg = serial16(lds, reg, uniform4(s.hc), int(s.ps - s.hbase), int(s.h0 - s.hbase));
   }
   if (kAlign && s.m) {
     // the chunks [ar, a1) right-aligned in lanes 8-m .. 7 (zeros before), the register entering at the first one;
@@ -418,7 +427,7 @@ __device__ __forceinline__ uint32_t finish(const uint8_t* lds, Staged<kG>& s, ui
     }
     reg = zmap(lds, kZ4Off, uint32_t(__builtin_amdgcn_readlane(int(p), 7)));  // register at a1
   }
-  if (kAbl != 3 && s.a1 < s.pe) {
+  if (Ext::kHeadTail && s.a1 < s.pe) {
     uint4 t = uniform4(s.tc);
     if (kPad && s.a1 == s.h0) t = mask_low(t, uint32_t(s.ps - s.h0));  // no body: the tail chunk is the first
     reg = serial16(lds, reg, t, 0, int(s.pe - s.a1));
@@ -682,19 +691,15 @@ __device__ __forceinline__ void fill_lds_compact(uint8_t* lds, const uint32_t* r
 // One workgroup per CU in every case (the LDS image is 157 KiB).
 // kVerify: the verify form -- each whole block this kernel emits is checked against a.expect (verify_uniform); the
 // pieces of split blocks are checked by the combine kernel, which produces their CRC.
-// kStrided (diag variants 27 / 28, static): a sweeping deal -- wave v takes items v, v + nwaves, v + 2 nwaves, ..., so
-// at any time the waves stream neighbouring pieces of one window that moves through the batch; its descriptor windows
-// hold the wave's next 64 items of that stride, resolved as in the contiguous modes.  v is numbered workgroup-major
-// (kStrided 1: a CU's waves on neighbouring pieces) or wave-major (2: neighbouring pieces on different CUs and XCDs).
-template <bool kPlanned, bool kDynamic, int kG, bool kNT, bool kAhead, int kAbl = 0, int kThreads = kWgThreads,
-          bool kAlign = true, bool kVerify = false, int kStrided = 0>
+// Ext: Exact (the shipped steps; the KVSEP_DIAG build's other types, crc32c_diag.inc, are its A/B forms and ablations).
+template <bool kPlanned, bool kDynamic, int kG, bool kNT, bool kAhead, int kThreads = kWgThreads, bool kAlign = true,
+          bool kVerify = false, typename Ext = Exact>
 __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
-  static_assert(!(kStrided && kDynamic), "the sweeping deal is static");
   constexpr uint32_t kWavesPerWg = kThreads / 64;
-  // the padded head (stage<kPad>); diag variant 26 (kAbl == 6) keeps the serial head of rounds 1-3 for A/B: measured
-  // 3a -0.8 / -1.8 %, config 4 -0.1 / -0.2 %, 3b and config 4's short blocks equal, in one process on two boxes
+  // the padded head (stage<kPad>); diag variant 26 keeps the serial head of rounds 1-3 for A/B: measured 3a -0.8 /
+  // -1.8 %, config 4 -0.1 / -0.2 %, 3b and config 4's short blocks equal, in one process on two boxes
   // (profiles/round4/pad_variant/)
-  constexpr bool kPad = kAbl != 6;
+  constexpr bool kPad = Ext::kPad;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   const uint32_t tid = threadIdx.x;
   KVSEP_WSTAMP_ENTRY();  // stamp hooks (crc32c_hooks.inc): empty in the shipped library
@@ -735,13 +740,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
     gdiv = total / (64 * nwaves);
     gdiv = gdiv < 4 ? 4 : gdiv > 32 ? 32 : gdiv;
   }
-  const uint64_t istep = kStrided ? nwaves : 1;  // item stride inside a descriptor window
   auto grab = [&]() -> bool {
-    if (kStrided) {
-      if (lo != ~uint64_t(0)) return false;
-      lo = kStrided == 1 ? uint64_t(blockIdx.x) * kWavesPerWg + wave : uint64_t(wave) * gridDim.x + blockIdx.x;
-      hi = total;
-    } else if (kDynamic) {
+    if (kDynamic) {
       const uint64_t rem = total > seen ? total - seen : 0;
       uint64_t c = rem / (gdiv * nwaves);
       if (a.guided_cap && c > a.guided_cap) c = a.guided_cap;
@@ -772,10 +772,10 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   uint32_t w_b = 0, w_reg0 = 0, w_only = 0, w_exp = 0;
   auto fill_set = [&](uint64_t start, uint64_t n, uintptr_t& w_ps, uintptr_t& w_pe, uint32_t& w_b, uint32_t& w_reg0,
                       uint32_t& w_only, uint32_t& w_exp) {
-    const uint64_t g = start + lane * istep;
+    const uint64_t g = start + lane;
     w_ps = w_pe = 0;
     w_b = w_reg0 = w_only = w_exp = 0;
-    if (kStrided ? lane < n : g < start + n) {
+    if (g < start + n) {
       uint64_t b, rs, re;
       bool first, only;
       if (planned) {
@@ -806,7 +806,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   };
   auto fill = [&](uint64_t start, uint64_t stop) {
     w0 = start;
-    const uint64_t left = kStrided ? (stop - start + istep - 1) / istep : stop - start;
+    const uint64_t left = stop - start;
     wn = left < 64 ? left : 64;
     fill_set(w0, wn, w_ps, w_pe, w_b, w_reg0, w_only, w_exp);
   };
@@ -816,7 +816,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
     bool only;
   };
   auto take = [&](uint64_t g, Item& it, Staged<kG>& st) {  // item g of the window -> stage its loads
-    const uint32_t i = kStrided ? uint32_t(g - w0) / uint32_t(istep) : uint32_t(g - w0);
+    const uint32_t i = uint32_t(g - w0);
     // readlane returns int: go through uint32_t so nothing is sign-extended into the upper half
     auto rl = [i](uint32_t v) -> uint32_t { return uint32_t(__builtin_amdgcn_readlane(int(v), int(i))); };
     it.g = g;
@@ -842,16 +842,16 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   // roles of the two buffers (ping-pong) instead of copying B into A after each item: such a copy must wait
   // for ALL of B's loads (vmcnt(0)) and would put a full HBM latency back on every item.
   auto step = [&](uint64_t g, uint64_t end, Item& ia, Staged<kG>& A, Item& ib, Staged<kG>& B) {
-    const bool hn = g + istep < end;
+    const bool hn = g + 1 < end;
     KVSEP_WSTAMP_ITEM_BEGIN();
     // The next item's HBM loads overlap the end of this item's compute (finish() stages them late, see
     // there).  The take is unconditional (the last item re-stages itself): on a path without it, this item's loads would be the most recent ones and the
     // compiler's counted wait (which merges both paths) would drain everything, vmcnt(0), on every item.
-    emit(ia, finish<kG, kNT, kAbl, kAlign, kPad>(lds, A, ia.reg0, lane, lc0, lc1, [&]() {
-           if (kAhead) take(hn ? g + istep : g, ib, B);
+    emit(ia, finish<kG, kNT, kAlign, kPad, Ext>(lds, A, ia.reg0, lane, lc0, lc1, [&]() {
+           if (kAhead) take(hn ? g + 1 : g, ib, B);
          }));
     KVSEP_WSTAMP_ITEM_END(ia);
-    if (!kAhead && hn) take(g + istep, ib, B);
+    if (!kAhead && hn) take(g + 1, ib, B);
     return hn;
   };
 
@@ -861,13 +861,13 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
   __syncthreads();
   KVSEP_WSTAMP_FILLED();
   while (grab()) {
-    for (uint64_t ws = lo; ws < hi; ws += 64 * istep) {
+    for (uint64_t ws = lo; ws < hi; ws += 64) {
       fill(ws, hi);
-      const uint64_t end = w0 + wn * istep;
+      const uint64_t end = w0 + wn;
       take(w0, cur, S);
-      for (uint64_t g = w0;; g += 2 * istep) {
+      for (uint64_t g = w0;; g += 2) {
         if (!step(g, end, cur, S, nxt, T)) break;
-        if (!step(g + istep, end, nxt, T, cur, S)) break;
+        if (!step(g + 1, end, nxt, T, cur, S)) break;
       }
     }
   }
@@ -954,8 +954,8 @@ __device__ __forceinline__ void nstage(NStaged<kG>& s, uintptr_t ps, uint32_t le
 // Raw register after the slot item, valid in the slot's last lane (j == 7).  kmin / kmax: wave min / max of K.
 // `next()` stages the following group, after this group's last row loads (see the wide kernel's finish()).
 // kL: lanes per slot, 8 (Z_128 rows, a 3-level slot tree) or 16 (diag: Z_256 rows, 4 levels; LdsFull only).
-template <int kG, bool kNT, int kAbl = 0, bool kAlign = true, typename Lay = LdsFull, int kL = kNarrowLanes,
-          typename Next>  // kAbl != 0: ablation (wrong)
+template <int kG, bool kNT, bool kAlign = true, typename Lay = LdsFull, int kL = kNarrowLanes, typename Ext = Exact,
+          typename Next>
 __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, uint32_t reg, uint32_t j,
                                             uint32_t lc0, uint32_t lc1, uint32_t kmin, uint32_t kmax,
                                             uintptr_t dummy, Next&& next) {
@@ -975,14 +975,10 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
     uint32_t c0 = v.x, c1 = v.y, c2 = v.z, c3 = v.w;
 #define KVSEP_NROW(V)                                                 \
   do {                                                                \
-    if (kAbl) {                                                       \
-      c0 ^= (V).x; c1 ^= (V).y; c2 ^= (V).z; c3 ^= (V).w;             \
-    } else {                                                          \
-      c0 = Lay::fold(lds, c0, (V).x, lc0, lc1);                       \
-      c1 = Lay::fold(lds, c1, (V).y, lc0, lc1);                       \
-      c2 = Lay::fold(lds, c2, (V).z, lc0, lc1);                       \
-      c3 = Lay::fold(lds, c3, (V).w, lc0, lc1);                       \
-    }                                                                 \
+    c0 = Ext::template nfold<Lay>(lds, c0, (V).x, lc0, lc1);          \
+    c1 = Ext::template nfold<Lay>(lds, c1, (V).y, lc0, lc1);          \
+    c2 = Ext::template nfold<Lay>(lds, c2, (V).z, lc0, lc1);          \
+    c3 = Ext::template nfold<Lay>(lds, c3, (V).w, lc0, lc1);          \
   } while (0)
     uint32_t r = 1;
     for (; r + 2 * kG <= kmin; r += kG) {  // every slot has rows r .. r+2kG-1: no guards, no clamps
@@ -1135,7 +1131,7 @@ __device__ __forceinline__ void narrow_deferred(const PiecesArgs& a, const uint8
             km = km > kk ? km : kk;
             kn = kn < kk ? kn : kk;
           }
-          uint32_t reg = nfinish<kG, kNT, 0, kAlignN, Lay, kL>(lds, X, p == 0 ? ~binit : 0u, j, lc0, lc1, kn, km, dummy,
+          uint32_t reg = nfinish<kG, kNT, kAlignN, Lay, kL>(lds, X, p == 0 ? ~binit : 0u, j, lc0, lc1, kn, km, dummy,
                                                          NoMid());
           if (j == kL - 1) reg = gf2_shift(a.tabs, reg, L - re);  // carried to the block's end
 #pragma unroll
@@ -1155,8 +1151,8 @@ __device__ __forceinline__ void narrow_deferred(const PiecesArgs& a, const uint8
 // workgroups than fit at once is the same computation (the hardware dispatcher then hands out the runs).
 // kVerify: the verify form (verify_wave after each group; the stored words are loaded just before the next group's
 // staging).
-template <int kG, bool kNT, int kThreads, bool kOverlap = false, int kAbl = 0, bool kAlignN = true,
-          typename Lay = LdsFull, bool kVerify = false>
+template <int kG, bool kNT, int kThreads, bool kOverlap = false, bool kAlignN = true, typename Lay = LdsFull,
+          bool kVerify = false, typename Ext = Exact>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   __shared__ __attribute__((aligned(16))) uint8_t lds[Lay::kBytes];
@@ -1245,8 +1241,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
       ex = ld32(a.expect + g + (slot < last ? slot : uint32_t(last)));
       __builtin_amdgcn_sched_barrier(0);
     }
-    const uint32_t reg = nfinish<kG, kNT, kAbl, kAlignN, Lay>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
-                                                           [&]() { take(gn, ib, B); });
+    const uint32_t reg = nfinish<kG, kNT, kAlignN, Lay, kNarrowLanes, Ext>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin,
+                                                                         ia.kmax, dummy, [&]() { take(gn, ib, B); });
     const bool mine = j == kNarrowLanes - 1 && g + slot < hi && !ia.over;
     // compare before the store: a store between the stored word's load and its wait (in a branch the wait must also
     // cover when skipped) would make that wait one count short and hold up the next group's first staged load
@@ -1398,7 +1394,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_claim_kernel(PiecesArg
       ex = ld32(a.expect + g0 + (slot < last ? slot : uint32_t(last)));
       __builtin_amdgcn_sched_barrier(0);
     }
-    const uint32_t reg = nfinish<kG, true, 0, true, LdsFull, kL>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
+    const uint32_t reg = nfinish<kG, true, true, LdsFull, kL>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
                                                     [&]() { take(gn, ib, B); });
     const bool mine = j == kL - 1 && g0 + slot < count && !ia.over;
     if (kVerify) verify_wave(a, lane, mine, g0, slot, ~reg, ex);  // before the store
@@ -1470,11 +1466,9 @@ __device__ __forceinline__ void wave_sort64(uint32_t& key, uint32_t& idx, uint32
 // slot s takes the block at sorted position 8k + s (two ds_bpermutes to find it, four to fetch its descriptor).
 // The rows, the slot tree and the end path are the narrow kernel's (nstage / nfinish); blocks over the hint go to
 // narrow_deferred as there.
-// kDrain: diag, vmcnt(0) after each group's emit.  kVIn (diag): 1 = the compare inside the kernel as before round 2
-// (load expected[b], compare, atomics); 2 = only the load of expected[b], folded into nothing; 3 / 4 = 1 plus s_nops /
-// a full s_waitcnt after the emit's join; 5 = 1 with a plain store in place of the atomics; 6 = the compare in full
-// EXEC (load, compare, ballot) with the atomics behind a wave-uniform branch (tools/sorted_vin_bisect.py)
-template <int kG, bool kNT, int kThreads, bool kDrain = false, int kVIn = 0, bool kVerify = false>
+// Ext::sorted_emit / sorted_join / kDrain: empty in Exact; the KVSEP_DIAG build's types put the round-3 bisection's
+// compare variants there (crc32c_diag.inc, tools/sorted_vin_bisect.py).
+template <int kG, bool kNT, int kThreads, bool kVerify = false, typename Ext = Exact>
 __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesArgs a) {
   constexpr uint32_t kWavesPerWg = kThreads / 64;
   constexpr uint32_t kPerGroup = 64 / kNarrowLanes;
@@ -1582,7 +1576,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesAr
         ex = ld32(a.expect + ia.w + (ia.live ? ia.src : 0u));
         __builtin_amdgcn_sched_barrier(0);
       }
-      const uint32_t reg = nfinish<kG, kNT, 0, true>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy, [&]() {
+      const uint32_t reg = nfinish<kG, kNT, true>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy, [&]() {
         if (here) {
           take(W, cw, k + 1, ib, B);
         } else if (next_win) {
@@ -1595,10 +1589,10 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesAr
       if (kVerify) verify_wave(a, lane, j == kNarrowLanes - 1 && ia.live, ia.w, ia.src, ~reg, ex);  // before the store
       if (j == kNarrowLanes - 1 && ia.live) {
         emit_block(a, ia.w + ia.src, ~reg);
-        diag_sorted_emit<kVIn>(a, ia.w + ia.src, reg);  // diag build only (crc32c_hooks.inc)
+        Ext::sorted_emit(a, ia.w + ia.src, reg);
       }
-      diag_sorted_join<kVIn>(a, j == kNarrowLanes - 1 && ia.live, ia.w, ia.src, reg, lane);
-      if (kDrain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      Ext::sorted_join(a, j == kNarrowLanes - 1 && ia.live, ia.w, ia.src, reg, lane);
+      if (Ext::kDrain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (here) {
         ++k;
         return true;
@@ -1783,8 +1777,6 @@ struct kvsep_crc32c_ctx {
   int dynamic = -1;  // -1 auto, 0 static, 1 guided
   int kernel = 0;    // kvsep_crc32c_ctx_set_kernel: 0 auto (use_narrow), 1 wide only, 2-6 narrow when the hint allows
   uint32_t static_contig = 1;  // static schedule: contiguous runs (1) or round-robin items (0, set_schedule(2))
-  int variant = 1;   // KVSEP_DIAG builds only: A/B and ablation variants of the wide kernel (launch_pieces_v)
-  int narrow = 1;    // KVSEP_DIAG builds only: narrow-kernel variants
   Scratch sc;  // scratch of the calls made directly on this context (any stream, event-ordered)
   int host_node = -1;        // NUMA node of the device's PCI function (-1: unknown / not bound): host legs go there
   bool inject_failure = false;  // kvsep_crc32c_ctx_inject_failure: the next call fails right after its CRC kernel
@@ -1797,8 +1789,8 @@ struct kvsep_crc32c_ctx {
   std::mutex mu;
 };
 
-// The KVSEP_DIAG tools build's launch variants and host hooks; in the shipped library the hooks are constant-false
-// inline functions (no variant is reachable, no environment variable is read).
+// The KVSEP_DIAG tools build's kernel variants, their per-context selection and host hooks; in the shipped library the
+// hooks are constant-false inline functions (no variant exists, no environment variable is read).
 #include "crc32c_diag.inc"
 
 namespace {
@@ -2034,7 +2026,7 @@ hipEvent_t take_event(kvsep_crc32c_ctx* c) {
 }
 
 template <bool P, bool D, bool V>
-void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs& a) {
+void launch_pieces_v(const kvsep_crc32c_ctx* c, unsigned grid, hipStream_t s, const PiecesArgs& a) {
   // Default (1): 8-wave workgroups (2 waves per SIMD, up to 256 VGPRs), 4-row groups, non-temporal loads, next
   // item staged ahead.  On one MI355X, interleaved in one process (tools/ab_variants.py), 8 waves beat 16 waves
   // by 1.5-2 % on 1 MiB blocks and by 4-5 % on the Zipf batch; 12 waves sit between.  (A 3-slot ring of row groups,
@@ -2043,28 +2035,29 @@ void launch_pieces_v(int variant, unsigned grid, hipStream_t s, const PiecesArgs
   // variants live in crc32c_diag.inc, compiled into the KVSEP_DIAG tools build only.
   constexpr int T = kWgThreads;
   if (V) {  // the verify form: the shipped configuration only
-    crc32c_pieces_kernel<P, D, 4, true, true, 0, T, true, true><<<grid, T, 0, s>>>(a);
+    crc32c_pieces_kernel<P, D, 4, true, true, T, true, true><<<grid, T, 0, s>>>(a);
     return;
   }
-  if (diag_launch_pieces<P, D>(variant, grid, s, a)) return;  // KVSEP_DIAG build only
-  crc32c_pieces_kernel<P, D, 4, true, true, 0, T><<<grid, T, 0, s>>>(a);
+  if (diag_launch_pieces<P, D>(c, grid, s, a)) return;  // KVSEP_DIAG build only
+  crc32c_pieces_kernel<P, D, 4, true, true, T><<<grid, T, 0, s>>>(a);
 }
 
 template <bool V>
-void launch_pieces_vv(bool planned, bool dyn, int variant, unsigned grid, hipStream_t s, const PiecesArgs& a) {
+void launch_pieces_vv(const kvsep_crc32c_ctx* c, bool planned, bool dyn, unsigned grid, hipStream_t s,
+                      const PiecesArgs& a) {
   if (planned) {
-    if (dyn) launch_pieces_v<true, true, V>(variant, grid, s, a);
-    else launch_pieces_v<true, false, V>(variant, grid, s, a);
+    if (dyn) launch_pieces_v<true, true, V>(c, grid, s, a);
+    else launch_pieces_v<true, false, V>(c, grid, s, a);
   } else {
-    if (dyn) launch_pieces_v<false, true, V>(variant, grid, s, a);
-    else launch_pieces_v<false, false, V>(variant, grid, s, a);
+    if (dyn) launch_pieces_v<false, true, V>(c, grid, s, a);
+    else launch_pieces_v<false, false, V>(c, grid, s, a);
   }
 }
 
-void launch_pieces(bool planned, bool dyn, bool verify, int variant, unsigned grid, hipStream_t s,
+void launch_pieces(const kvsep_crc32c_ctx* c, bool planned, bool dyn, bool verify, unsigned grid, hipStream_t s,
                    const PiecesArgs& a) {
-  if (verify) launch_pieces_vv<true>(planned, dyn, variant, grid, s, a);
-  else launch_pieces_vv<false>(planned, dyn, variant, grid, s, a);
+  if (verify) launch_pieces_vv<true>(c, planned, dyn, grid, s, a);
+  else launch_pieces_vv<false>(c, planned, dyn, grid, s, a);
 }
 
 int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, bool capturing, const void* base,
@@ -2201,11 +2194,11 @@ int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, PiecesArg
     a.hint = max_len;
     if (expect && (nv == 6 || nv == 9 || nv == 10 || nv == 11 || nv == 20)) {  // verify form of the shipped forms
       switch (nv) {
-        case 9: crc32c_narrow_kernel<4, true, 512, true, 0, true, LdsFull, true><<<grid, 512, 0, s>>>(a); break;
+        case 9: crc32c_narrow_kernel<4, true, 512, true, true, LdsFull, true><<<grid, 512, 0, s>>>(a); break;
         case 10: crc32c_narrow_claim_kernel<4, 512, true><<<grid, 512, 0, s>>>(a); break;
         case 11: crc32c_narrow_claim_kernel<4, 512, true, true, 16><<<grid, 512, 0, s>>>(a); break;
-        case 20: crc32c_narrow_sorted_kernel<4, true, 1024, false, 0, true><<<grid, 1024, 0, s>>>(a); break;
-        default: crc32c_narrow_kernel<4, true, 1024, false, 0, true, LdsFull, true><<<grid, 1024, 0, s>>>(a); break;
+        case 20: crc32c_narrow_sorted_kernel<4, true, 1024, true><<<grid, 1024, 0, s>>>(a); break;
+        default: crc32c_narrow_kernel<4, true, 1024, false, true, LdsFull, true><<<grid, 1024, 0, s>>>(a); break;
       }
     } else {
     // KVSEP_DIAG variants only (the shipped forms are 6, 9, 10, 11 and 20): they post to the caller's words directly, from
@@ -2225,7 +2218,7 @@ int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, PiecesArg
     }
     }
   } else {
-    launch_pieces(planned, dyn, expect != nullptr, c->variant, grid, s, a);
+    launch_pieces(c, planned, dyn, expect != nullptr, grid, s, a);
   }
   KVSEP_HIP(hipGetLastError());
   if (c->inject_failure) {  // fault injection (tests): fail between the CRC kernel and the combine kernel
@@ -2320,6 +2313,7 @@ void kvsep_crc32c_ctx_destroy(kvsep_crc32c_ctx* c) {
   for (auto& p : c->ev_pending) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
   for (auto e : c->ev_pool) hipEventDestroy(e);
   release_staging(c->staging);
+  diag_forget(c);  // KVSEP_DIAG build only
   delete c;
 }
 

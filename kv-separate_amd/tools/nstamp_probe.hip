@@ -3,7 +3,8 @@
 // spread (p10 / p50 / p90 / max, us) of each stamp over all waves: where a small batch's time goes (launch ramp,
 // fill, first data, last-group compute tail).  Never used for timing numbers.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o nstamp_probe nstamp_probe.hip
-// Usage: nstamp_probe <block_len> <count> <kernel: 3 = narrow 16 waves, 4 = narrow 8 waves, 6 = claim>
+// Usage: nstamp_probe <block_len> <count> <kernel: 3 = narrow 16 waves, 4 = narrow 8 waves, 6 = claim,
+//                                              0 = the streaming-read ceiling over the same bytes>
 #define KVSEP_STAMPS 1
 #include "../csrc/crc32c_device.hip"
 #include "../csrc/crc32c_host.cpp"
@@ -12,6 +13,43 @@
 
 #include <algorithm>
 #include <vector>
+
+// kernel 0: stream_read_kernel (crc32c_device.hip) with the same per-wave stamps -- [0] entry, [1] the first round's
+// data in registers (its loads issued at entry: nothing to fill), [2..6] after rounds 2, 4, 8, 12, 16 of its 1 MiB
+// chunk, [7] exit -- so the CRC kernels' ramp and drain can be read against the streaming ceiling's own (round 5).
+__global__ void __launch_bounds__(512) stamped_stream_kernel(uintptr_t src, uint64_t n16, uint32_t* sink) {
+  using namespace kvsep;
+  constexpr uint32_t kWavesPerWg = 8;
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(w);
+  KVSEP_NSTAMP_ENTRY();
+  constexpr uint64_t kChunk16 = (1u << 20) / 16;
+  constexpr uint64_t kStep = 8 * kStreamRows * kRowBytes;
+  const uint64_t nchunks = n16 / kChunk16;
+  uint32_t acc = 0;
+  int round = 0;
+  for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const uintptr_t p = src + c * kChunk16 * 16 + uintptr_t(w) * kRowBytes + lane * 16u;
+#pragma unroll 1
+    for (uint64_t r = 0; r < kChunk16 * 16; r += kStep) {
+      uint4 v[kStreamRows];
+#pragma unroll
+      for (int u = 0; u < kStreamRows; ++u) v[u] = ld16<true>(p + r + uint64_t(u) * 8 * kRowBytes);
+#pragma unroll
+      for (int u = 0; u < kStreamRows; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+      ++round;
+      if (round == 1) {
+        asm volatile("" : "+v"(acc));
+        KVSEP_NSTAMP(1);
+      } else if (round == 2 || round == 4 || round == 8 || round == 12 || round == 16) {
+        asm volatile("" : "+v"(acc));
+        KVSEP_NSTAMP(round == 2 ? 2 : round == 4 ? 3 : round == 8 ? 4 : round == 12 ? 5 : 6);
+      }
+    }
+  }
+  KVSEP_NSTAMP(7);
+  if (acc == 0x9e3779b9u) atomicXor(sink, acc);
+}
 
 int main(int argc, char** argv) {
   const uint64_t blen = argc > 1 ? strtoull(argv[1], nullptr, 0) : 4096;
@@ -34,7 +72,10 @@ int main(int argc, char** argv) {
     hipEvent_t ev0, ev1;
     hipEventCreate(&ev0); hipEventCreate(&ev1);
     hipEventRecord(ev0, nullptr);
-    kvsep_crc32c_batch_device(ctx, nullptr, data, doff, dlen, nullptr, out, count, blen * count, blen);
+    if (kernel == 0)
+      stamped_stream_kernel<<<256, 512>>>(reinterpret_cast<uintptr_t>(data), blen * count / 16, out);
+    else
+      kvsep_crc32c_batch_device(ctx, nullptr, data, doff, dlen, nullptr, out, count, blen * count, blen);
     hipEventRecord(ev1, nullptr);
     hipDeviceSynchronize();
     float ms = 0;
@@ -46,6 +87,8 @@ int main(int argc, char** argv) {
       if (z[w * 8]) { t0 = std::min(t0, z[w * 8]); ++nw; }
     printf("rep %d: event %.2f us, %d waves\n", rep, ms * 1e3, nw);
     const char* names[8] = {"entry", "fill done", "group 1", "group 2", "group 3", "group 4", "group 5", "exit"};
+    const char* snames[8] = {"entry", "1st data", "round 2", "round 4", "round 8", "round 12", "round 16", "exit"};
+    if (kernel == 0) std::copy(snames, snames + 8, names);
     for (int k = 0; k < 8; ++k) {
       std::vector<double> v;
       for (int w = 0; w < 8192; ++w)

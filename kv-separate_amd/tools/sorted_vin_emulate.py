@@ -43,7 +43,8 @@ def main():
     stored = np.array([mask(int(x)) for x in exp], dtype=np.uint32)
     tabs = E.dev_tables()
     for v in args.variants.split(","):
-        name = "_ZN5kvsep27crc32c_narrow_sorted_kernelILi4ELb1ELi1024ELb0ELi%dELb0EEEvNS_10PiecesArgsE" % KVIN[v]
+        ext = "NS_5ExactE" if KVIN[v] == 0 else "NS_9SortedVInILi%dEEE" % KVIN[v]  # the Ext type (crc32c_diag.inc)
+        name = "_ZN5kvsep27crc32c_narrow_sorted_kernelILi4ELb1ELi1024ELb0E%sEEvNS_10PiecesArgsE" % ext
         t0 = time.time()
         # the diag variants read expect / first_bad / nbad themselves (kVerify false, kVIn > 0)
         out, written, fb, nb, steps = E.run_batch_kernel(args.asm, name, 1024, host, off, ln, tabs, wg=args.wg,

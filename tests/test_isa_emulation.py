@@ -28,9 +28,9 @@ sys.path.insert(0, PKG)
 # the shipped narrow-family templates (launch_batch_in in csrc/crc32c_device.hip): name, threads per workgroup.  The
 # claim kernel's waves take groups through an LDS counter; the emulator runs a workgroup's waves to each barrier in
 # order, so its deal differs from the hardware's (a different interleaving, the same set of groups)
-SORTED = "_ZN5kvsep27crc32c_narrow_sorted_kernelILi4ELb1ELi1024ELb0ELi0ELb%dEEEvNS_10PiecesArgsE"
-NARROW16 = "_ZN5kvsep20crc32c_narrow_kernelILi4ELb1ELi1024ELb0ELi0ELb1ENS_7LdsFullELb%dEEEvNS_10PiecesArgsE"
-NARROW8 = "_ZN5kvsep20crc32c_narrow_kernelILi4ELb1ELi512ELb1ELi0ELb1ENS_7LdsFullELb%dEEEvNS_10PiecesArgsE"
+SORTED = "_ZN5kvsep27crc32c_narrow_sorted_kernelILi4ELb1ELi1024ELb%dENS_5ExactEEEvNS_10PiecesArgsE"
+NARROW16 = "_ZN5kvsep20crc32c_narrow_kernelILi4ELb1ELi1024ELb0ELb1ENS_7LdsFullELb%dENS_5ExactEEEvNS_10PiecesArgsE"
+NARROW8 = "_ZN5kvsep20crc32c_narrow_kernelILi4ELb1ELi512ELb1ELb1ENS_7LdsFullELb%dENS_5ExactEEEvNS_10PiecesArgsE"
 CLAIM = "_ZN5kvsep26crc32c_narrow_claim_kernelILi4ELi512ELb%dELb1ELi8EEEvNS_10PiecesArgsE"
 CLAIM16 = "_ZN5kvsep26crc32c_narrow_claim_kernelILi4ELi512ELb%dELb1ELi16EEEvNS_10PiecesArgsE"
 # (label, template, threads per workgroup, arrival levels of the verify publish: 8 = per-XCD shards, then the final word)
@@ -111,7 +111,7 @@ def _verify_tail(E, name, threads, data, off, ln, tabs, wg, hint, exp, mask, min
     assert st["vacc"] == (int(plant.min()), final, *sh), [hex(v) for v in st["vacc"]]
 
 
-PIECES = "_ZN5kvsep20crc32c_pieces_kernelILb%dELb%dELi4ELb1ELb1ELi0ELi512ELb1ELb%dELi0EEEvNS_10PiecesArgsE"
+PIECES = "_ZN5kvsep20crc32c_pieces_kernelILb%dELb%dELi4ELb1ELb1ELi512ELb1ELb%dENS_5ExactEEEvNS_10PiecesArgsE"
 COMBINE = "_ZN5kvsep21crc32c_combine_kernelILb%dEEEvNS_10PiecesArgsE"
 
 

@@ -125,3 +125,24 @@ def test_audit_catches_a_missing_wait(built, tmp_path):
             blocks, succ = A.parse_function(body)
             hits += len(A.audit(blocks, succ, "inorder"))
     assert hits > 0
+
+
+def test_shipped_kernels_are_exact_only(built):
+    """the kernel templates' replaceable steps come from an Ext type, and the shipped library has
+    one, Exact -- the A/B forms and the ablations (wrong results by design) are types only the KVSEP_DIAG build
+    defines (csrc/crc32c_diag.inc).  Every shipped CRC kernel is instantiated with Exact, and no diag type's name, nor
+    the integer switches they replaced, is anywhere in the shipped assembly or the shipped kernel source."""
+    asm, _ = built
+    text = open(asm).read()
+    names = set(re.findall(r"_ZN5kvsep\d+crc32c_(?:pieces|narrow|narrow_sorted)_kernel\w+", text))
+    assert len(names) == 14, names  # 8 wide (planned x guided x verify), 4 narrow, 2 sorted
+    assert all("NS_5ExactE" in n for n in names), [n for n in names if "NS_5ExactE" not in n]
+    for diag_type in ("AblNoMerge", "AblXorRows", "AblNoHeadTail", "AblNoTree", "AblFreeShort", "SerialHead",
+                      "SortedVIn", "SortedDrain"):
+        assert diag_type not in text, diag_type
+    src = open(os.path.join(PKG, "csrc", "crc32c_device.hip")).read()
+    for switch in ("kAbl", "kStrided", "kVIn", "c->variant", "c->narrow"):
+        assert switch not in src, switch
+    diag = open(os.path.join(PKG, "csrc", "crc32c_diag.inc")).read()
+    head, shipped = diag.split("#else  // the shipped library", 1)
+    assert "struct AblXorRows" in head and "struct" not in shipped  # the types live in the KVSEP_DIAG half only
