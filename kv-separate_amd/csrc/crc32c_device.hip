@@ -973,6 +973,7 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
     uint4 v = (K && rel0 >= int32_t(g.h0)) ? s.v : make_uint4(0, 0, 0, 0);
     if (K && rel0 == int32_t(g.h0)) v.x ^= reg;  // the head register enters as pending word at h0
     uint32_t c0 = v.x, c1 = v.y, c2 = v.z, c3 = v.w;
+    KVSEP_NSTAMP_FIRST_DATA(c0);  // stamp hook (crc32c_hooks.inc): empty in the shipped library
 #define KVSEP_NROW(V)                                                 \
   do {                                                                \
     c0 = Ext::template nfold<Lay>(lds, c0, (V).x, lc0, lc1);          \

@@ -67,8 +67,9 @@ int main(int argc, char** argv) {
   hipMemcpy(doff, off.data(), count * 8, hipMemcpyHostToDevice);
   hipMemcpy(dlen, len.data(), count * 8, hipMemcpyHostToDevice);
   for (int rep = 0; rep < 4; ++rep) {
-    std::vector<unsigned long long> z(8192 * 8, 0);
+    std::vector<unsigned long long> z(8192 * 8, 0), f(8192, 0);
     hipMemcpyToSymbol(HIP_SYMBOL(kvsep::g_kvsep_stamps), z.data(), z.size() * 8);
+    hipMemcpyToSymbol(HIP_SYMBOL(kvsep::g_kvsep_first), f.data(), f.size() * 8);
     hipEvent_t ev0, ev1;
     hipEventCreate(&ev0); hipEventCreate(&ev1);
     hipEventRecord(ev0, nullptr);
@@ -81,6 +82,7 @@ int main(int argc, char** argv) {
     float ms = 0;
     hipEventElapsedTime(&ms, ev0, ev1);
     hipMemcpyFromSymbol(z.data(), HIP_SYMBOL(kvsep::g_kvsep_stamps), z.size() * 8);
+    hipMemcpyFromSymbol(f.data(), HIP_SYMBOL(kvsep::g_kvsep_first), f.size() * 8);
     unsigned long long t0 = ~0ull;
     int nw = 0;
     for (int w = 0; w < 8192; ++w)
@@ -98,6 +100,15 @@ int main(int argc, char** argv) {
       auto q = [&](double f) { return v[std::min(v.size() - 1, size_t(f * v.size()))]; };
       printf("  %-9s n=%5zu  p10 %7.2f  p50 %7.2f  p90 %7.2f  max %7.2f us\n", names[k], v.size(), q(0.1), q(0.5),
              q(0.9), v.back());
+      if (k == 1 && kernel != 0) {  // the narrow kernels' first HBM data (KVSEP_NSTAMP_FIRST_DATA)
+        std::vector<double> u;
+        for (int w = 0; w < 8192; ++w)
+          if (z[w * 8] && f[w]) u.push_back((f[w] - t0) / 100.0);
+        std::sort(u.begin(), u.end());
+        if (!u.empty())
+          printf("  %-9s n=%5zu  p10 %7.2f  p50 %7.2f  p90 %7.2f  max %7.2f us\n", "1st data", u.size(),
+                 u[u.size() / 10], u[u.size() / 2], u[u.size() * 9 / 10], u.back());
+      }
     }
     // exit time by XCD (workgroup id mod 8) and by wave slot within the workgroup: is the tail spatial?
     const int wpg = nw / 256 > 0 ? nw / 256 : 1;
