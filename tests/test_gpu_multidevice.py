@@ -288,3 +288,24 @@ def test_bench_self_launch_eight_ranks_config2_every_block():
     sm = line["per_rank_summary"]
     assert sm["ranks"] == 8 and sm["same_device_rehearsal"] and not sm["distinct_devices"], sm
     assert sm["GiBps_min"] <= sm["GiBps_max"] and 0 <= sm["GiBps_skew"] < 1 and sm["slowest_rank"] in range(8), sm
+
+
+def test_two_ranks_host_round_trip_per_rank_records():
+    """Two torchrun ranks on the one GPU with the host round trip on: each rank's record carries its own round-trip
+    rate and the NUMA node of its pinned image (the node of the rank's GPU, where the rank bound itself), and the
+    line's aggregate is the sum over ranks / the slowest rank."""
+    env = dict(os.environ, KVSEP_BENCH_SAME_DEVICE="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--no-cpu",
+           "--config", "2", "--steps", "3", "--warmup", "1", "--roundtrip-gib", "0.25"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["host_roundtrip_parity"] is True and line["host_roundtrip_ranks"] == 2, line
+    pr = line["per_rank"]
+    assert len(pr) == 2 and all(x["roundtrip_GiBps"] > 0 for x in pr), pr
+    node = pr[0]["numa_node"]
+    if node is not None and node >= 0:
+        assert all(x["roundtrip_image_numa_node"] == node for x in pr), pr
+        assert all(x["staging"]["device_node"] == node for x in pr), pr
+    assert line["host_roundtrip_GiBps"] <= sum(x["roundtrip_GiBps"] for x in pr) * 1.01, line
