@@ -455,7 +455,8 @@ def live_pmc_traffic(args, timeout_s=240):
     cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--pmc", "FETCH_SIZE", "--kernel-trace", "-d", d, "-o", "pmc",
            "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), "--config", args.config,
            "--steps", "3", "--warmup", "1", "--no-cpu", "--roundtrip-gib", "0", "--pmc-live", "off", "--launch", "eager",
-           "--schedule", args.schedule] + (["--piece-kib", str(args.piece_kib)] if args.piece_kib else []) + \
+           "--schedule", args.schedule, "--form", args.form] + \
+          (["--piece-kib", str(args.piece_kib)] if args.piece_kib else []) + \
           (["--no-plan-hint"] if args.no_plan_hint else [])
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
@@ -543,6 +544,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="CPU work per thread count (>= 1 pass)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--roundtrip-gib", type=float, default=4.0)
+    ap.add_argument("--form", default="batch", choices=["batch", "verify"],
+                    help="verify: each step is the verify form (Mask(crc) compared with stored words inside the CRC "
+                         "kernels, db/value_log_reader.cc:109-122) against the reference's words with 2 planted "
+                         "mismatches per rank; first_bad / nbad reduced over the ranks (all-reduce MIN / SUM)")
     ap.add_argument("--numa-bind", default="auto", choices=["auto", "off"],
                     help="auto: bind each rank's threads (and its pinned memory) to its GPU's NUMA node (place_rank)")
     ap.add_argument("--dry-run", action="store_true",
@@ -631,10 +636,36 @@ def main():
     out = torch.zeros((npass, max(count, 1)), dtype=torch.int32, device=dev)
     ctx.reserve(count, useful)
     stream = torch.cuda.current_stream()
+    verify = args.form == "verify"
+    planted = []
+    if verify:
+        if npass != 1 or not count:
+            raise SystemExit("--form verify needs a one-pass configuration (2, 3a, 3b, 4)")
+        ib = plan.passes[0][1]
+        gold = None
+        if plan.golden:
+            g = np.fromfile(os.path.join(GOLDEN, plan.golden), dtype="<u4")
+            if g.size >= ib + count:
+                gold = g[ib:ib + count]
+        if gold is None:  # no reference words for this range (config 4 past its first 2^20 blocks): the batch form's
+            ctx.batch_device(data.data_ptr(), d_off, d_len, out[0], count=count, total_bytes=useful, max_len=max_len)
+            torch.cuda.synchronize()  # (checked against the reference's digest below, like every result)
+            gold = out[0, :count].cpu().numpy().view(np.uint32).copy()
+        rot = (gold >> np.uint32(15)) | (gold << np.uint32(17))
+        stored = (rot + np.uint32(0xA282EAD8)).astype(np.uint32)  # Mask, util/crc32c.h:29-32
+        planted = sorted({(rank * 7919 + 13) % count, count - 1 - (rank * 31) % count})
+        stored[planted] ^= np.uint32(0x00010000)
+        d_expect = torch.from_numpy(stored.view(np.int32)).to(dev)
+        d_fb = torch.zeros(1, dtype=torch.int64, device=dev)
+        d_nb = torch.zeros(1, dtype=torch.int64, device=dev)
 
     def crc(p, st):
-        ctx.batch_device(data.data_ptr(), d_off, d_len, out[p], count=count, total_bytes=useful, max_len=max_len,
-                         stream=st)
+        if verify:
+            ctx.verify_device(data.data_ptr(), d_off, d_len, d_expect, out[p], d_fb, d_nb, count=count,
+                              total_bytes=useful, max_len=max_len, stream=st)
+        else:
+            ctx.batch_device(data.data_ptr(), d_off, d_len, out[p], count=count, total_bytes=useful, max_len=max_len,
+                             stream=st)
 
     # ---- warm-up
     for _ in range(args.warmup):
@@ -746,6 +777,20 @@ def main():
                             useful * npass * args.steps, kernel_name, launch_bytes=useful)
 
     # ---- outside the timed region: u32 results of every rank gathered (RCCL), every block checked
+    verdict = None
+    if verify:  # the last step's verdict, reduced over the ranks: the global lowest bad index and the total
+        fb, nb = int(d_fb.item()), int(d_nb.item())
+        local_first = -1 if fb in (-1, (1 << 64) - 1) else fb
+        ib = plan.passes[0][1]
+        gnb, gfb = shard.verify_over_ranks(nb, -1 if local_first < 0 else ib + local_first, dd, coll_dev)
+        want = [(r, Plan(args.config, world, r)) for r in range(world)]
+        exp_first = min(pl.passes[0][1] + min({(r * 7919 + 13) % pl.count, pl.count - 1 - (r * 31) % pl.count})
+                        for r, pl in want if pl.count)
+        exp_n = sum(len({(r * 7919 + 13) % pl.count, pl.count - 1 - (r * 31) % pl.count}) for r, pl in want if pl.count)
+        verdict = {"first_bad": gfb, "nbad": gnb, "planted_per_rank": len(planted), "expected_first_bad": exp_first,
+                   "expected_nbad": exp_n, "ok": gfb == exp_first and gnb == exp_n,
+                   "reduction": "all-reduce MIN of first_bad (global index) and SUM of nbad over the ranks"
+                   if dd else "one rank"}
     crcs = out[:, :count].cpu().numpy().view(np.uint32).reshape(-1)
     results = shard.gather_results(crcs, dd, coll_dev)
     digests = [shard.crc_of_crcs(r, kvsep.extend_host) for r in results]
@@ -953,6 +998,8 @@ def main():
             "digests": [hex(d) for d in digests],
             "per_rank": per_rank,
             "per_rank_summary": shard.rank_summary(per_rank, same_device=same_device),
+            "form": args.form,
+            "verify": verdict,
         }
         print(json.dumps(line), flush=True)
     ctx.close()

@@ -106,6 +106,24 @@ def sum_over_ranks(value: float, dist, device) -> float:
     return float(t.item())
 
 
+def verify_over_ranks(nbad: int, first_bad: int, dist, device) -> tuple[int, int]:
+    """The verify form across ranks: total mismatches (all-reduce SUM) and the lowest mismatching GLOBAL
+    block index (all-reduce MIN; each rank's first_bad already offset by its index base, -1 = none) -- what a reader
+    that stops at the first bad record needs (db/value_log_reader.cc:109-122), and the reduction
+    kvsep_crc32c_group_verify_device does between the members of one process.  Identity with no process group."""
+    import torch
+
+    if not _active(dist):
+        return nbad, first_bad
+    big = np.iinfo(np.int64).max
+    n = torch.tensor([nbad], dtype=torch.int64, device=device)
+    f = torch.tensor([big if first_bad < 0 else first_bad], dtype=torch.int64, device=device)
+    dist.all_reduce(n, op=dist.ReduceOp.SUM)
+    dist.all_reduce(f, op=dist.ReduceOp.MIN)
+    fb = int(f.item())
+    return int(n.item()), (-1 if fb == big else fb)
+
+
 def gather_objects(obj, dist) -> list:
     """All-gather one picklable object per rank (the per-rank records of a bench line) -> the list in rank order on
     every rank; [obj] with no process group.  Over RCCL (the nccl backend) the pickled bytes travel as a device

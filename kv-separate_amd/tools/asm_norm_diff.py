@@ -1,3 +1,8 @@
+#!/usr/bin/env python3
+"""Two builds' gfx950 assembly (build/crc32c_device-hip-amdgcn-amd-amdhsa-gfx950.s), compared instruction by
+instruction: comments, directives and labels dropped, kvsep symbol names and basic-block labels normalised (a template
+parameter list that changes a kernel's mangled name changes nothing else).  Prints both instruction counts, the
+number of differing lines and the first hunks.  usage: asm_norm_diff.py <old.s> <new.s>"""
 import re, sys
 def norm(path):
     out = []

@@ -309,3 +309,30 @@ def test_two_ranks_host_round_trip_per_rank_records():
         assert all(x["roundtrip_image_numa_node"] == node for x in pr), pr
         assert all(x["staging"]["device_node"] == node for x in pr), pr
     assert line["host_roundtrip_GiBps"] <= sum(x["roundtrip_GiBps"] for x in pr) * 1.01, line
+
+
+@pytest.mark.parametrize("config", ["2", "3a"])
+def test_two_ranks_verify_form_reduction(config):
+    """`bench.py --form verify` at two ranks: every rank verifies its shard against the reference's words, two planted
+    mismatches per rank, and the global first_bad / nbad after the cross-rank reduction.  (Config 4 is 150 GiB per
+    rank: two ranks do not fit one GPU; its verify form runs at one rank below.)"""
+    line = _torchrun_bench(2, "--config", config, "--steps", "2", "--warmup", "1", "--form", "verify")
+    v = line["verify"]
+    assert v["ok"] and v["nbad"] == 4 and v["first_bad"] == 13, v
+    assert line["parity"]["mismatches"] == 0 and line["parity"]["mismatching_digest_ranges"] == 0, line["parity"]
+
+
+def test_verify_form_config4_one_rank():
+    """Config 4's verify form (ragged Zipf blocks: the planned wide kernel, the combine kernel publishing the verdict)
+    against the reference's words for its 2^20 blocks."""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "KVSEP_BENCH_SAME_DEVICE"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", "4", "--steps", "2", "--warmup", "1",
+           "--no-cpu", "--roundtrip-gib", "0", "--pmc-live", "off", "--form", "verify"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    v = line["verify"]
+    assert v["ok"] and v["nbad"] == 2 and v["first_bad"] == 13, v
+    assert line["parity"]["mismatches"] == 0 and line["parity"]["every_block_checked"], line["parity"]

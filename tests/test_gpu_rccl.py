@@ -99,3 +99,19 @@ def test_bench_torchrun_one_rank_rccl():
     assert pr[0]["kernel_avg_ms"] > 0 and pr[0]["GiBps"] > 0 and pr[0]["roundtrip_GiBps"] > 0, pr
     sm = line["per_rank_summary"]
     assert sm["ranks"] == 1 and sm["distinct_devices"] and sm["pci_bus_ids"] == [bdf], sm
+
+
+def test_bench_verify_form_one_rank_rccl():
+    """`--form verify` through bench's RCCL path: each step is the verify form against the reference's stored words
+    with two planted mismatches, and the verdict goes through the all-reduce MIN / SUM of SURVEY.md §8e."""
+    env = _env()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+           "127.0.0.1", "--master-port", env["MASTER_PORT"], os.path.join(ROOT, "bench.py"), "--gpus", "1", "--config",
+           "2", "--steps", "4", "--warmup", "1", "--no-cpu", "--pmc-live", "off", "--roundtrip-gib", "0",
+           "--form", "verify"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    v = line["verify"]
+    assert line["form"] == "verify" and v["ok"] and v["nbad"] == 2 and v["first_bad"] == 13, v
+    assert line["parity"]["mismatches"] == 0 and line["parity"]["every_block_checked"], line["parity"]

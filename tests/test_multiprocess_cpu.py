@@ -35,15 +35,9 @@ def gather_digests(digest: int, dist, device) -> list[int]:
 
 
 def reduce_verify(nbad: int, first_bad: int, dist, device) -> tuple[int, int]:
-    """Verify mode across ranks: total mismatches and the lowest mismatching GLOBAL block index (first_bad already
-    offset by the rank's index base; -1 means none) -- the reduction kvsep_crc32c_group_verify_device does in-process."""
-    big = np.iinfo(np.int64).max
-    n = torch.tensor([nbad], dtype=torch.int64, device=device)
-    f = torch.tensor([big if first_bad < 0 else first_bad], dtype=torch.int64, device=device)
-    dist.all_reduce(n, op=dist.ReduceOp.SUM)
-    dist.all_reduce(f, op=dist.ReduceOp.MIN)
-    fb = int(f.item())
-    return int(n.item()), (-1 if fb == big else fb)
+    """Verify mode across ranks: kvsep.shard.verify_over_ranks (bench.py --form verify runs the same reduction)."""
+    from kvsep import shard
+    return shard.verify_over_ranks(nbad, first_bad, dist, device)
 
 
 def _worker(rank, world, port, q):
