@@ -17,8 +17,12 @@
 // kernel 0: stream_read_kernel (crc32c_device.hip) with the same per-wave stamps -- [0] entry, [1] the first round's
 // data in registers (its loads issued at entry: nothing to fill), [2..6] after rounds 2, 4, 8, 12, 16 of its 1 MiB
 // chunk, [7] exit -- so the CRC kernels' ramp and drain can be read against the streaming ceiling's own (round 5).
+// kLds (kernel 5): the same kernel holding the CRC kernels' 157 KiB LDS image (unused), to see whether a workgroup that
+// takes a whole CU's LDS is dispatched later than one that takes none.
+template <bool kLds>
 __global__ void __launch_bounds__(512) stamped_stream_kernel(uintptr_t src, uint64_t n16, uint32_t* sink) {
   using namespace kvsep;
+  __shared__ uint8_t lds_pad[kLds ? kLdsBytes : 16];
   constexpr uint32_t kWavesPerWg = 8;
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(w);
@@ -48,7 +52,11 @@ __global__ void __launch_bounds__(512) stamped_stream_kernel(uintptr_t src, uint
     }
   }
   KVSEP_NSTAMP(7);
-  if (acc == 0x9e3779b9u) atomicXor(sink, acc);
+  if (acc == 0x9e3779b9u) {
+    lds_pad[threadIdx.x] = uint8_t(acc);
+    __syncthreads();
+    atomicXor(sink, acc ^ lds_pad[threadIdx.x ^ 1u]);
+  }
 }
 
 int main(int argc, char** argv) {
@@ -74,7 +82,9 @@ int main(int argc, char** argv) {
     hipEventCreate(&ev0); hipEventCreate(&ev1);
     hipEventRecord(ev0, nullptr);
     if (kernel == 0)
-      stamped_stream_kernel<<<256, 512>>>(reinterpret_cast<uintptr_t>(data), blen * count / 16, out);
+      stamped_stream_kernel<false><<<256, 512>>>(reinterpret_cast<uintptr_t>(data), blen * count / 16, out);
+    else if (kernel == 5)
+      stamped_stream_kernel<true><<<256, 512>>>(reinterpret_cast<uintptr_t>(data), blen * count / 16, out);
     else
       kvsep_crc32c_batch_device(ctx, nullptr, data, doff, dlen, nullptr, out, count, blen * count, blen);
     hipEventRecord(ev1, nullptr);
@@ -90,7 +100,7 @@ int main(int argc, char** argv) {
     printf("rep %d: event %.2f us, %d waves\n", rep, ms * 1e3, nw);
     const char* names[8] = {"entry", "fill done", "group 1", "group 2", "group 3", "group 4", "group 5", "exit"};
     const char* snames[8] = {"entry", "1st data", "round 2", "round 4", "round 8", "round 12", "round 16", "exit"};
-    if (kernel == 0) std::copy(snames, snames + 8, names);
+    if (kernel == 0 || kernel == 5) std::copy(snames, snames + 8, names);
     for (int k = 0; k < 8; ++k) {
       std::vector<double> v;
       for (int w = 0; w < 8192; ++w)
@@ -100,7 +110,7 @@ int main(int argc, char** argv) {
       auto q = [&](double f) { return v[std::min(v.size() - 1, size_t(f * v.size()))]; };
       printf("  %-9s n=%5zu  p10 %7.2f  p50 %7.2f  p90 %7.2f  max %7.2f us\n", names[k], v.size(), q(0.1), q(0.5),
              q(0.9), v.back());
-      if (k == 1 && kernel != 0) {  // the narrow kernels' first HBM data (KVSEP_NSTAMP_FIRST_DATA)
+      if (k == 1 && kernel != 0 && kernel != 5) {  // the narrow kernels' first HBM data (KVSEP_NSTAMP_FIRST_DATA)
         std::vector<double> u;
         for (int w = 0; w < 8192; ++w)
           if (z[w * 8] && f[w]) u.push_back((f[w] - t0) / 100.0);
