@@ -1882,12 +1882,14 @@ int ensure_verify(Scratch& sc) {
 
 // Puts accumulator set `line` back in its reset state, in stream order (capturable: two memsets).  Needed after a call
 // that failed once its CRC kernel was enqueued: the kernel's posts stay in the set, and with no publishing kernel after
-// them nothing resets it -- the next verdict would inherit a stale count and first_bad.
-int reset_vacc(Scratch& sc, uint32_t line, hipStream_t s) {
+// them nothing resets it -- the next verdict would inherit a stale count and first_bad.  Under capture the
+// memsets only become graph nodes that may never run, so the set stays marked (every later captured call on it resets
+// it first, at the cost of two memset nodes) until an eager call has reset it.
+int reset_vacc(Scratch& sc, uint32_t line, hipStream_t s, bool capturing) {
   unsigned long long* v = vacc_set(sc, line);
   KVSEP_HIP(hipMemsetAsync(v, 0, kVaccSetWords * 8, s));
   KVSEP_HIP(hipMemsetAsync(v, 0xff, 8, s));
-  sc.vacc_dirty &= ~(1u << line);
+  if (!capturing) sc.vacc_dirty &= ~(1u << line);
   return KVSEP_OK;
 }
 
@@ -2109,7 +2111,7 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, bool captur
     if (rc) return rc;
     line = capturing ? 1 + (sc.vacc_next++ % (kVaccLines - 1)) : 0;
     if (sc.vacc_dirty & (1u << line)) {
-      rc = reset_vacc(sc, line, s);
+      rc = reset_vacc(sc, line, s, capturing);
       if (rc) return rc;
     }
     a.vacc = vacc_set(sc, line);  // the accumulators, in their reset state: the kernels publish the verdict
