@@ -9,7 +9,7 @@ linked with the real util/crc32c.cc produced tests/golden/ref_framing.json (test
 the files must be byte-identical (SHA-256) and every reader verdict -- records returned, bytes reported dropped
 and why -- identical.
 
-CPU: the drop-in's host leg (every call below the offload threshold).  GPU: threshold 0, so every Extend -- down to
+CPU: the drop-in's host leg (every call below the offload threshold), on each of its three legs.  GPU: threshold 0, so every Extend -- down to
 log_writer.cc's 1-byte InitTypeCrc calls -- runs through the GPU, and the driver fails if any call finished on
 the host."""
 import hashlib
@@ -29,9 +29,13 @@ def _gold():
         return json.load(f)
 
 
-def _run(tmp_path, gpu):
+def _run(tmp_path, gpu, host_leg=None):
     args = [DRIVER, str(tmp_path)] + (["gpu"] if gpu else [])
-    r = subprocess.run(args, capture_output=True, text=True, timeout=600)
+    env = dict(os.environ)
+    env.pop("KVSEP_HOST_CRC", None)
+    if host_leg:
+        env["KVSEP_HOST_CRC"] = host_leg
+    r = subprocess.run(args, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
     return json.loads(r.stdout), r.stderr
 
@@ -46,8 +50,10 @@ def _check(j, tmp_path):
 
 
 @pytest.mark.skipif(not os.path.exists(DRIVER), reason="oracle/_ref not built here (needs /root/reference)")
-def test_reference_callsites_on_engine_host_leg(tmp_path):
-    j, err = _run(tmp_path, gpu=False)
+@pytest.mark.parametrize("host_leg", [None, "sse42", "portable"])
+def test_reference_callsites_on_engine_host_leg(tmp_path, host_leg):
+    """On each host leg (round 5: the portable leg that non-x86 hosts and x86 CPUs without SSE4.2 run, too)."""
+    j, err = _run(tmp_path, gpu=False, host_leg=host_leg)
     _check(j, tmp_path)
     assert "0 gpu calls" in err
 
