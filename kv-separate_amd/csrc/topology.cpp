@@ -50,6 +50,7 @@ int kvsep_numa_node_cpus(int node, int* cpus, int cap) {
 }
 
 int kvsep_bind_process_numa(int node) {
+  if (node < 0 || node >= kvsep::numa::kMaxNodes) return 0;
   const std::vector<int> cpus = kvsep::numa::node_cpus_allowed(node, kvsep::numa::thread_cpus());
   if (cpus.empty()) return 0;
   // every thread that exists now (the HIP runtime's among them); threads created later inherit from their creator
