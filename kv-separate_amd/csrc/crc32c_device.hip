@@ -461,29 +461,39 @@ __device__ uint32_t gf2_shift(const DevTables* tabs, uint32_t reg, uint64_t n) {
 __device__ __forceinline__ void emit_block(const PiecesArgs& a, uint64_t b, uint32_t crc) { a.out[b] = crc; }
 
 // The verify form's accumulators (PiecesArgs::vacc, u64 words, each group on a 128-B line of its own): [0] the lowest
-// mismatching block (~0: none); [1] the final arrival word, (arrivals << 40) | mismatches: every mismatch count is
-// posted there, so the count travels with the arrivals; and at [16 (s + 1)] the arrival word of shard s = blockIdx.x
+// mismatching block (~0: none); [1] the final arrival word, (arrivals << 40) | mismatches: every mismatch count ends
+// up there, so the count travels with the arrivals; and at [16 (s + 1)] the arrival word of shard s = blockIdx.x
 // mod 8 (one shard per XCD: the dispatcher deals workgroups round-robin over the 8 XCDs), used by grids whose
 // workgroups arrive together (verify_publish).
 constexpr uint32_t kVaccShards = 8, kVaccStride = 16;  // 16 words = 128 B
 constexpr unsigned long long kArrive = 1ull << 40, kCountMask = kArrive - 1;
 
-// A wave that posted a mismatch waits, right there, until its posts are performed (the rare path: it drains the wave's
-// staged loads once), so the end of the kernel needs no wait before the workgroup arrives (verify_publish): a clean
-// workgroup arrives while its last result stores are still in flight.  Atomic against atomic, a completed post is all
-// the order needs.  Not __threadfence(): on gfx950 that is an L2 writeback + invalidate (buffer_wbl2 / buffer_inv sc1),
-// which at the end of every wave cost 130-170 us per launch (measured).
+// A workgroup that saw a mismatch waits until its lowest-block post is performed before it arrives (verify_publish);
+// a clean workgroup arrives while its last result stores are still in flight.  Atomic against atomic, a completed post
+// is all the order needs.  Not __threadfence(): on gfx950 that is an L2 writeback + invalidate (buffer_wbl2 /
+// buffer_inv sc1), which at the end of every wave cost 130-170 us per launch (measured).
 __device__ __forceinline__ void post_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// The verify form's running verdict of one wave: its lowest mismatching block and its mismatch count, wave-uniform
+// (scalar registers).  Round 5: a wave no longer posts each group's mismatches with global atomics as it goes (two
+// atomics on one 128-B line per group, and a vmcnt(0) that drained the next group's staged rows): on an image where
+// every block is bad that serialised ~16 K atomics on one line and ran 4x the clean call (217 vs 52 us, 65,536 blocks
+// of 4 KiB).  The wave keeps its verdict here; the workgroup combines its waves' verdicts at the end and posts once
+// (verify_publish / verify_post).
+struct VAcc {
+  uint64_t best = ~0ull;
+  uint32_t cnt = 0;
+};
 
 // The verify form fused into the CRC kernels (db/value_log_reader.cc:109-122, table/format.cc:99-106).  Called by the
 // whole wave (full EXEC) right after a group's emit: lanes with `mine` hold block b's crc and the stored word `ex`
 // they loaded before the next group's staging (so waiting for it never drains those loads).  The compare itself is
-// branch-free; the wave ballots the mismatches and only a mismatch enters a wave-uniform branch, where one lane posts
-// the wave's lowest mismatching index (vacc[0]) and the count (vacc[1]).  A per-lane branch on the
-// compare nested inside the emit's divergent branch is what made the round-1 sorted-window kernel miscompute (DESIGN
-// §3.5).  The lane's block is base + idx (base wave-uniform): one VGPR for the index, not a 64-bit pair.
-__device__ __forceinline__ void verify_wave(const PiecesArgs& a, uint32_t lane, bool mine, uint64_t base, uint32_t idx,
-                                            uint32_t crc, uint32_t ex) {
+// branch-free; the wave ballots the mismatches and only a mismatch enters a wave-uniform branch, which folds the
+// lowest mismatching index and the count into the wave's verdict.  A per-lane branch on the compare nested inside the
+// emit's divergent branch is what made the round-1 sorted-window kernel miscompute.  The lane's block
+// is base + idx (base wave-uniform): one VGPR for the index, not a 64-bit pair.
+__device__ __forceinline__ void verify_wave(VAcc& acc, bool mine, uint64_t base, uint32_t idx, uint32_t crc,
+                                            uint32_t ex) {
   const uint64_t m = __builtin_amdgcn_ballot_w64(mine && mask_crc(crc) != ex);
   if (m) {  // wave-uniform
     uint32_t best = ~0u;
@@ -491,22 +501,49 @@ __device__ __forceinline__ void verify_wave(const PiecesArgs& a, uint32_t lane, 
       const uint32_t il = uint32_t(__builtin_amdgcn_readlane(int(idx), __builtin_ctzll(t)));
       best = il < best ? il : best;
     }
-    if (lane == 0) {
-      atomicMin(a.vacc, (unsigned long long)(base + best));
-      atomicAdd(a.vacc + 1, (unsigned long long)__builtin_popcountll(m));
-    }
-    post_wait();
+    const uint64_t b = base + best;
+    acc.best = b < acc.best ? b : acc.best;
+    acc.cnt += uint32_t(__builtin_popcountll(m));
   }
 }
 
 // One block checked by a whole wave whose crc and stored word are wave-uniform (the wide kernel, the deferred walk).
-__device__ __forceinline__ void verify_uniform(const PiecesArgs& a, uint32_t lane, uint64_t b, uint32_t crc,
-                                               uint32_t ex) {
-  if (mask_crc(crc) != ex && lane == 0) {
-    atomicMin(a.vacc, (unsigned long long)b);
-    atomicAdd(a.vacc + 1, 1ull);
-    post_wait();
+__device__ __forceinline__ void verify_uniform(VAcc& acc, uint64_t b, uint32_t crc, uint32_t ex) {
+  if (mask_crc(crc) != ex) {  // wave-uniform
+    acc.best = b < acc.best ? b : acc.best;
+    acc.cnt += 1;
   }
+}
+
+// The workgroup's verdict from its waves' (every wave calls it, full EXEC): each wave's lane 0 leaves its verdict in
+// the workgroup's LDS slots, a barrier, then wave 0 reads them all.  Only wave 0's return value is the workgroup's.
+template <uint32_t kWaves>
+__device__ __forceinline__ VAcc verify_gather(const VAcc& acc, uint32_t wave, uint32_t lane) {
+  __shared__ unsigned long long v_best[kWaves];
+  __shared__ uint32_t v_cnt[kWaves];
+  if (lane == 0) {
+    v_best[wave] = acc.best;
+    v_cnt[wave] = acc.cnt;
+  }
+  __syncthreads();  // every wave of the workgroup is done with its groups
+  VAcc wg;
+  if (wave == 0) {
+#pragma unroll
+    for (uint32_t w = 0; w < kWaves; ++w) {
+      const unsigned long long b = v_best[w];
+      wg.best = b < wg.best ? b : wg.best;
+      wg.cnt += v_cnt[w];
+    }
+  }
+  return wg;
+}
+
+// The lane, recomputed (v_mbcnt) rather than kept live from the kernel's start: at the 16-wave kernels' 128-VGPR cap
+// one more long-lived VGPR spills.
+__device__ __forceinline__ uint32_t lane_id() {
+  uint32_t lane;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+  return lane;
 }
 
 // One returning device-scope atomic add by lane 0, its old value broadcast (wave-uniform).
@@ -518,38 +555,57 @@ __device__ __forceinline__ unsigned long long arrive(unsigned long long* w, unsi
 }
 
 // The end of a publishing verify kernel (the CRC kernel of an unsplit batch, the combine kernel of a split one), every
-// workgroup: once its waves are done with their posts, wave 0 arrives on the final word; the last workgroup to arrive
-// copies the verdict to the caller's first_bad / nbad and puts the accumulators back in their reset state (~0, 0) for
-// the next call.  So a verify call needs no init launch, and a clean batch costs its last workgroup one atomic round
-// trip (vacc[0] is read, and reset, only when something mismatched).
+// workgroup: the workgroup's verdict (verify_gather); if it saw mismatches, wave 0 posts its lowest index (vacc[0],
+// and waits for it), then arrives with its count added to the arrival: the last workgroup to arrive copies the verdict
+// to the caller's first_bad / nbad and puts the accumulators back in their reset state (~0, 0) for the next call.  So
+// a verify call needs no init launch, a clean batch costs its last workgroup one atomic round trip (vacc[0] is read,
+// and reset, only when something mismatched), and a batch full of bad blocks one atomicMin per workgroup.
 // kShards = 8: the workgroups arrive first on their shard's word and only each shard's last on the final word.  For a
 // grid whose workgroups all arrive at once (the combine kernel): 256 arrivals on ONE word queue at ~11-13 ns each
 // (MI355X_MICROARCH.md fanin: 3.2-4.5 us; measured +2.7 us on the combine kernel).  The CRC kernels' workgroups end
 // over several us (issue-age staircase), so they take one level: one round trip less for the last one.
 // `wave`: the wave's index in the workgroup (wave-uniform, an SGPR); the lane is recomputed here (v_mbcnt) rather than
 // kept live from the kernel's start: at the 16-wave kernels' 128-VGPR cap one more long-lived VGPR spills.
-template <uint32_t kShards = 1>
-__device__ __forceinline__ void verify_publish(const PiecesArgs& a, uint32_t wave) {
-  __syncthreads();  // every wave of the workgroup is done; any that posted has waited for its posts (post_wait)
+template <uint32_t kWaves, uint32_t kShards = 1>
+__device__ __forceinline__ void verify_publish(const PiecesArgs& a, uint32_t wave, const VAcc& acc) {
+  const uint32_t lane = lane_id();
+  const VAcc wg = verify_gather<kWaves>(acc, wave, lane);
   if (wave != 0) return;
-  uint32_t lane;
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+  if (wg.cnt) {  // wave-uniform: the workgroup's lowest bad block lands before its arrival is counted
+    if (lane == 0) atomicMin(a.vacc, (unsigned long long)wg.best);
+    post_wait();
+  }
+  unsigned long long add = kArrive + wg.cnt;  // the count travels with the arrival
   uint32_t arrivals = gridDim.x;  // expected on the final word
   if (kShards > 1) {
     const uint32_t shard = blockIdx.x % kShards;
     unsigned long long* sw = a.vacc + kVaccStride * (1 + shard);
-    const unsigned long long o1 = arrive(sw, kArrive, lane);
+    const unsigned long long o1 = arrive(sw, add, lane);
     if ((o1 >> 40) + 1 != (gridDim.x - shard + kShards - 1) / kShards) return;  // not the shard's last
     if (lane == 0) atomicExch(sw, 0ull);  // the shard word back to its reset state
+    add = kArrive + (o1 & kCountMask) + wg.cnt;  // the shard's count: its earlier workgroups' and this one's
     arrivals = gridDim.x < kShards ? gridDim.x : kShards;
   }
-  const unsigned long long old = arrive(a.vacc + 1, kArrive, lane);
+  const unsigned long long old = arrive(a.vacc + 1, add, lane);
   if ((old >> 40) + 1 != arrivals || lane != 0) return;  // the last workgroup of all, lane 0
-  const unsigned long long nb = old & kCountMask;
+  const unsigned long long nb = (old & kCountMask) + (add & kCountMask);
   atomicExch(a.vacc + 1, 0ull);  // first, so the wait for the swap's result below is a plain vmcnt(0)
   const unsigned long long fb = nb ? atomicExch(a.vacc, ~0ull) : ~0ull;
   *a.first_bad = fb;
   *a.nbad = nb;
+}
+
+// The end of a verify CRC kernel that does not publish (the wide kernel of a split batch: the combine kernel after it
+// publishes): the workgroup's verdict goes to the accumulators directly -- its lowest bad block and its count on the
+// final word, where the combine kernel's arrivals find them (the kernel boundary orders them).
+template <uint32_t kWaves>
+__device__ __forceinline__ void verify_post(const PiecesArgs& a, uint32_t wave, const VAcc& acc) {
+  const uint32_t lane = lane_id();
+  const VAcc wg = verify_gather<kWaves>(acc, wave, lane);
+  if (wave == 0 && wg.cnt && lane == 0) {
+    atomicMin(a.vacc, (unsigned long long)wg.best);
+    atomicAdd(a.vacc + 1, (unsigned long long)wg.cnt);
+  }
 }
 
 // A 32-bit global load (address space 1), for the stored words of the verify form.
@@ -828,14 +884,14 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
     const uintptr_t pe = (uintptr_t(rl(uint32_t(w_pe >> 32))) << 32) | uintptr_t(rl(uint32_t(w_pe)));
     stage<kG, kNT, kAlign, kPad>(st, ps, pe, lane, reinterpret_cast<uintptr_t>(a.tabs), vz);
   };
+  VAcc vacc;  // the verify form's verdict of this wave
   auto emit = [&](const Item& it, uint32_t reg) {
     if (lane == 0) {
       if (it.only) emit_block(a, it.b, ~reg);
       else a.partial[it.g] = reg;
     }
     // lane 0 holds the register: its readlane makes the compare, and the branch on it, wave-uniform
-    if (kVerify && it.only)
-      verify_uniform(a, lane, it.b, ~uint32_t(__builtin_amdgcn_readlane(int(reg), 0)), it.exp);
+    if (kVerify && it.only) verify_uniform(vacc, it.b, ~uint32_t(__builtin_amdgcn_readlane(int(reg), 0)), it.exp);
   };
 
   // One item: finish item g (staged in A) while item g+1 is staged into B.  The loop below alternates the
@@ -872,7 +928,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_pieces_kernel(PiecesArgs a) {
     }
   }
   KVSEP_WSTAMP_EXIT();
-  if (kVerify && !kPlanned) verify_publish(a, wave);  // a split batch's verdict is the combine kernel's to publish
+  if (kVerify && !kPlanned) verify_publish<kWavesPerWg>(a, wave, vacc);
+  if (kVerify && kPlanned) verify_post<kWavesPerWg>(a, wave, vacc);  // the combine kernel publishes a split batch's
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1075,7 +1132,7 @@ __device__ __forceinline__ uint32_t nfinish(const uint8_t* lds, NStaged<kG>& s, 
 // main path (long blocks are not what the narrow kernels are for) but exact for any 64-bit length.
 template <int kG, bool kNT, bool kAlignN, typename Lay = LdsFull, bool kVerify = false, int kL = kNarrowLanes>
 __device__ __forceinline__ void narrow_deferred(const PiecesArgs& a, const uint8_t* lds, uint64_t lo, uint64_t hi,
-                                                uintptr_t dummy) {
+                                                uintptr_t dummy, VAcc& vacc) {
   constexpr uint32_t kPerGroup = 64 / kL;
   // The lane constants are recomputed here (volatile, so not merged with the kernel's own): values kept live across
   // the main group loop for this rarely taken walk would cost registers at the 16-wave kernels' 128-VGPR cap.
@@ -1141,7 +1198,7 @@ __device__ __forceinline__ void narrow_deferred(const PiecesArgs& a, const uint8
         }
         if (lane == 0) emit_block(a, g + k, ~acc);
         // acc is wave-uniform (a readlane sum); so is the stored word, read through readfirstlane
-        if (kVerify) verify_uniform(a, lane, g + k, ~acc, uint32_t(__builtin_amdgcn_readfirstlane(int(ld32(a.expect + g + k)))));
+        if (kVerify) verify_uniform(vacc, g + k, ~acc, uint32_t(__builtin_amdgcn_readfirstlane(int(ld32(a.expect + g + k)))));
       }
     }
   }
@@ -1209,6 +1266,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
   };
   Desc dn;  // descriptors of the next group to take
   bool deferred = false;  // wave-uniform: some block of this wave's run exceeded the hint
+  VAcc vacc;              // the verify form's verdict of this wave
   const uint32_t hint32 = uint32_t(a.hint);  // <= 64 KiB (use_narrow)
   auto take = [&](uint64_t g, NItem& it, NStaged<kG>& st) {
     const bool in = g + slot < hi;
@@ -1247,7 +1305,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     const bool mine = j == kNarrowLanes - 1 && g + slot < hi && !ia.over;
     // compare before the store: a store between the stored word's load and its wait (in a branch the wait must also
     // cover when skipped) would make that wait one count short and hold up the next group's first staged load
-    if (kVerify) verify_wave(a, lane, mine, g, slot, ~reg, ex);
+    if (kVerify) verify_wave(vacc, mine, g, slot, ~reg, ex);
     if (mine) emit_block(a, g + slot, ~reg);
     load_desc(gn + kPerGroup, dn);  // here, where this group's registers are dead
     return gn < hi;
@@ -1292,8 +1350,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_kernel(PiecesArgs a) {
     }
   }
   KVSEP_NSTAMP(7);
-  if (deferred) narrow_deferred<kG, kNT, kAlignN, Lay, kVerify>(a, lds, lo, hi, dummy);
-  if (kVerify) verify_publish(a, wave);
+  if (deferred) narrow_deferred<kG, kNT, kAlignN, Lay, kVerify>(a, lds, lo, hi, dummy, vacc);
+  if (kVerify) verify_publish<kWavesPerWg>(a, wave, vacc);
 }
 
 // Batches of short blocks up to ~1 GiB (narrow_form 10, round 4): the workgroup owns a contiguous run of 8-block
@@ -1387,6 +1445,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_claim_kernel(PiecesArg
     it.kmin = kn;
   };
   uint32_t gn = kNone;  // the group staged next (its descriptors are in dn until its take)
+  VAcc vacc;            // the verify form's verdict of this wave
   auto step = [&](CItem& ia, NStaged<kG>& A, CItem& ib, NStaged<kG>& B) -> bool {
     const uint64_t g0 = uint64_t(ia.g) * kPerGroup;
     uint32_t ex = 0;
@@ -1398,11 +1457,11 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_claim_kernel(PiecesArg
     const uint32_t reg = nfinish<kG, true, true, LdsFull, kL>(lds, A, ia.reg0, j, lc0, lc1, ia.kmin, ia.kmax, dummy,
                                                     [&]() { take(gn, ib, B); });
     const bool mine = j == kL - 1 && g0 + slot < count && !ia.over;
-    if (kVerify) verify_wave(a, lane, mine, g0, slot, ~reg, ex);  // before the store
+    if (kVerify) verify_wave(vacc, mine, g0, slot, ~reg, ex);  // before the store
     if (mine) emit_block(a, g0 + slot, ~reg);
     if (ia.deferred)  // wave-uniform: this group's blocks over the hint, whole
       narrow_deferred<kG, true, true, LdsFull, kVerify, kL>(a, lds, g0, g0 + kPerGroup < count ? g0 + kPerGroup : count,
-                                                        dummy);
+                                                        dummy, vacc);
     gn = next_group();  // the group after ib: claimed now, its descriptors loaded while ib runs
     load_desc(gn, dn);
     return ib.g != kNone;
@@ -1437,7 +1496,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_claim_kernel(PiecesArg
   KVSEP_NSTAMP(7);
   // two-level arrival: the claims balance the run, so the 256 workgroups end within a µs of each other (bunched, as
   // the combine kernel's do), unlike the other narrow forms' staircase of workgroup ends
-  if (kVerify) verify_publish<kVaccShards>(a, wave);
+  if (kVerify) verify_publish<kWaves, kVaccShards>(a, wave, vacc);
 }
 
 // Bitonic sort of one (key, idx) pair per lane over the wavefront, ascending by key (ties by idx, so the two
@@ -1515,6 +1574,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesAr
     bool live;
   };
   bool deferred = false;
+  VAcc vacc;  // the verify form's verdict of this wave
   auto take = [&](uint64_t W, const WDesc& d, uint32_t k, NItem& it, NStaged<kG>& st) {
     uint32_t sl = slot;
     asm volatile("" : "+v"(sl));  // see load_desc in crc32c_narrow_kernel
@@ -1587,7 +1647,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesAr
           take_empty(ib, B);
         }
       });
-      if (kVerify) verify_wave(a, lane, j == kNarrowLanes - 1 && ia.live, ia.w, ia.src, ~reg, ex);  // before the store
+      if (kVerify) verify_wave(vacc, j == kNarrowLanes - 1 && ia.live, ia.w, ia.src, ~reg, ex);  // before the store
       if (j == kNarrowLanes - 1 && ia.live) {
         emit_block(a, ia.w + ia.src, ~reg);
         Ext::sorted_emit(a, ia.w + ia.src, reg);
@@ -1612,8 +1672,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_narrow_sorted_kernel(PiecesAr
       if (!step(nxt, T, cur, S)) break;
     }
   }
-  if (deferred) narrow_deferred<kG, kNT, true, LdsFull, kVerify>(a, lds, lo, hi, dummy);
-  if (kVerify) verify_publish(a, wave);
+  if (deferred) narrow_deferred<kG, kNT, true, LdsFull, kVerify>(a, lds, lo, hi, dummy, vacc);
+  if (kVerify) verify_publish<kWavesPerWg>(a, wave, vacc);
 }
 
 // One thread per block: Horner over the block's pieces, R <- Z_piece(R) ^ R_piece.  kVerify: also the verify form's
@@ -1639,8 +1699,9 @@ __global__ void __launch_bounds__(256) crc32c_combine_kernel(PiecesArgs a) {
     emit_block(a, b, crc);
   }
   if (kVerify) {
-    verify_wave(a, threadIdx.x & 63u, mine, uint64_t(blockIdx.x) * 256, threadIdx.x, crc, ld32(a.expect + bb));
-    verify_publish<kVaccShards>(a, threadIdx.x >> 6);  // after the CRC kernel's whole-block posts
+    VAcc vacc;
+    verify_wave(vacc, mine, uint64_t(blockIdx.x) * 256, threadIdx.x, crc, ld32(a.expect + bb));
+    verify_publish<4, kVaccShards>(a, threadIdx.x >> 6, vacc);  // after the CRC kernel's whole-block posts
   }
 }
 

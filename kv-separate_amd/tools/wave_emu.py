@@ -496,6 +496,15 @@ class Workgroup:
             w.sset(o[0], r & M32)
             w.scc = int(r < -(1 << 31) or r >= (1 << 31))
             return
+        if op in ('s_addk_i32', 's_mulk_i32'):  # sdst op= sign-extended 16-bit immediate
+            a, k16 = g(o[0]), g(o[1]) & 0xFFFF
+            sa = a - (1 << 32) if a >> 31 else a
+            sk = k16 - 0x10000 if k16 & 0x8000 else k16
+            r = sa + sk if op == 's_addk_i32' else sa * sk
+            w.sset(o[0], r & M32)
+            if op == 's_addk_i32':
+                w.scc = int(r < -(1 << 31) or r >= (1 << 31))
+            return
         if op == 's_mul_i32':
             w.sset(o[0], (g(o[1]) * g(o[2])) & M32)
             return
@@ -643,6 +652,17 @@ class Workgroup:
             a = w.vget(o[1]).astype(np.int64) + off
             w.vset(o[0], self.lds_read32(a, act))
             return
+        if op in ('ds_read_b64', 'ds_read_b96', 'ds_read_b128'):  # wider reads (the verify form's slot reads, round 5)
+            n = {'ds_read_b64': 2, 'ds_read_b96': 3, 'ds_read_b128': 4}[op]
+            a = w.vget(o[1]).astype(np.int64) + off
+            m = REG.match(o[0])
+            first = int(m.group(2)) if m.group(1) else int(m.group(4))
+            for l in np.nonzero(act)[0]:
+                ad = int(a[l])
+                vals = struct.unpack('<%dI' % n, self.lds[ad:ad + 4 * n].tobytes())
+                for i in range(n):
+                    w.v[first + i][l] = vals[i]
+            return
         if op in ('ds_write_b32', 'ds_write_b64', 'ds_write_b128'):
             n = {'ds_write_b32': 1, 'ds_write_b64': 2, 'ds_write_b128': 4}[op]
             a = w.vget(o[0]).astype(np.int64) + off
@@ -665,6 +685,16 @@ class Workgroup:
                 self.lds[ad:ad + 4] = np.frombuffer(struct.pack('<I', (cur + int(data[l])) & M32), dtype=np.uint8)
             if ret:
                 w.vset(o[0], old_vals)
+            return
+        if op in ('ds_min_u32', 'ds_min_u64'):  # non-returning LDS atomic min (the verify form's slot, round 5)
+            x2 = op == 'ds_min_u64'
+            a = w.vget(o[0]).astype(np.int64) + off
+            data = w.vget(o[1], 64) if x2 else w.vget(o[1])
+            fmt, nb = ('<Q', 8) if x2 else ('<I', 4)
+            for l in np.nonzero(act)[0]:
+                ad = int(a[l])
+                cur = struct.unpack(fmt, self.lds[ad:ad + nb].tobytes())[0]
+                self.lds[ad:ad + nb] = np.frombuffer(struct.pack(fmt, min(cur, int(data[l]))), dtype=np.uint8)
             return
         if op == 'ds_bpermute_b32':
             addr = w.vget(o[1]).astype(np.int64) + off

@@ -103,11 +103,12 @@ def _verify_tail(E, name, threads, data, off, ln, tabs, wg, hint, exp, mask, min
     *_, fb, nb, _ = E.run_batch_kernel(ASM, name, threads, data, off, ln, tabs, wg=wg, hint=hint, expect=stored,
                                        lds_bytes=lds_bytes, last=False, state=st, shards=shards)
     assert (fb, nb) == (E.SENTINEL, E.SENTINEL)  # not published
-    # the count on the final word; the arrival there (one level) or on the workgroup's shard word (two levels)
+    # the workgroup's count travels with its arrival (round 5): on the final word (one level) or on the workgroup's
+    # shard word (two levels); its lowest bad block on vacc[0]
     sh = [0] * E.VACC_SHARDS
     if shards > 1:
-        sh[wg % shards] = 1 << 40
-    final = len(plant) | ((1 << 40) if shards == 1 else 0)
+        sh[wg % shards] = (1 << 40) | len(plant)
+    final = (len(plant) | (1 << 40)) if shards == 1 else 0
     assert st["vacc"] == (int(plant.min()), final, *sh), [hex(v) for v in st["vacc"]]
 
 
