@@ -86,6 +86,11 @@ def test_emulated_kernel_matches_oracle(env, label, tmpl, threads, shards, kind)
     assert np.array_equal(np.nonzero(written_v)[0], mine)
     assert np.array_equal(out_v[mine], exp[mine])
     assert (fb, nb) == (int(plant.min()), 3)  # published by this (last) workgroup, accumulators reset (batch_results)
+    if kind == "short":  # every block of the workgroup bad: every wave's verdict, several mismatches per wave
+        bad = np.array([mask(int(x)) for x in exp], np.uint32) ^ np.uint32(0x100)
+        *_, fb, nb, _ = E.run_batch_kernel(ASM, tmpl % 1, threads, data, off, ln, tabs, wg=wg, hint=hint, expect=bad,
+                                           shards=shards)
+        assert (fb, nb) == (int(mine.min()), int(mine.size))
     _verify_tail(E, tmpl % 1, threads, data, off, ln, tabs, wg, hint, exp, mask, mine, plant, shards=shards)
 
 
