@@ -241,6 +241,52 @@ def test_verify_mode_first_bad(ctx, oracle):
     assert fb.item() == 41 and nb.item() == 2
 
 
+@pytest.mark.parametrize("kernel,shape", [("wide", "4k"), ("narrow16", "4k"), ("narrow8", "4k"), ("claim", "4k"),
+                                          ("claim16", "8k"), ("sorted", "ragged"), ("auto", "split")])
+def test_verify_every_block_bad(kernel, shape, oracle):
+    """A batch whose every stored word is wrong (a corrupt table or vlog, table/format.cc:99-106): the verdict is block
+    0 and the whole count, on every kernel form and through the combine kernel of a split batch.  Round 5 posts one
+    verdict per workgroup (crc32c_device.hip verify_publish), where round 4 posted per group with a mismatch."""
+    c = kvsep.Context(0)
+    try:
+        c.set_kernel(kernel)
+        if shape == "4k":
+            ln = np.full(20000, 4096, np.uint64)
+        elif shape == "8k":
+            ln = np.full(8192, 8192, np.uint64)
+        elif shape == "ragged":
+            ln = np.random.default_rng(3).integers(1, 9000, 30000).astype(np.uint64)
+        else:  # blocks over the piece size: split, the combine kernel publishes
+            ln = np.random.default_rng(4).integers(100, 3 << 20, 300).astype(np.uint64)
+        off = np.zeros(ln.size, np.uint64)
+        off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+        span = int(off[-1] + ln[-1])
+        d = torch.empty(span + 64, dtype=torch.uint8, device=DEV)
+        kvsep.fill_splitmix64(d.data_ptr(), span, 21, 0)
+        out = torch.zeros(ln.size, dtype=torch.int32, device=DEV)
+        fb = torch.zeros(1, dtype=torch.int64, device=DEV)
+        nb = torch.zeros(1, dtype=torch.int64, device=DEV)
+        args = dict(total_bytes=int(ln.sum()), max_len=int(ln.max()))
+        want_kernel = {"wide": "pieces", "narrow16": "narrow_kernel", "narrow8": "narrow_kernel", "claim": "claim",
+                       "claim16": "claim", "sorted": "sorted", "auto": "pieces"}[kernel]
+        assert want_kernel in c.kernel_name(ln.size, args["max_len"], args["total_bytes"])
+        c.batch_device(d.data_ptr(), dev_u64(off), dev_u64(ln), out, **args)
+        torch.cuda.synchronize()
+        crc = out.cpu().numpy().view(np.uint32).copy()
+        sample = np.linspace(0, ln.size - 1, 64).astype(np.int64)
+        host = d[:span].cpu().numpy()
+        assert np.array_equal(crc[sample], oracle.batch(host, off[sample], ln[sample], threads=8))
+        good = np.array([oracle.lib.oracle_crc32c_mask(int(x)) for x in crc], np.uint32)
+        for flip, want in ((np.uint32(0x100), (0, ln.size)), (np.uint32(0), (-1, 0))):  # all bad, then clean again
+            c.verify_device(d.data_ptr(), dev_u64(off), dev_u64(ln), dev_u32(good ^ flip), out, fb, nb, **args)
+            torch.cuda.synchronize()
+            assert (fb.item(), nb.item()) == want, (kernel, shape, flip)
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), crc)
+        del d
+    finally:
+        c.close()
+
+
 def test_host_span_and_gather_forms(ctx, oracle):
     off, ln = W.cfg4_layout(3000)
     span = int(off[-1] + ln[-1])
