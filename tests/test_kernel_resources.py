@@ -140,7 +140,8 @@ def test_shipped_kernels_are_exact_only(built):
     for diag_type in ("AblNoMerge", "AblXorRows", "AblNoHeadTail", "AblNoTree", "AblFreeShort", "SerialHead",
                       "SortedVIn", "SortedDrain"):
         assert diag_type not in text, diag_type
-    src = open(os.path.join(PKG, "csrc", "crc32c_device.hip")).read()
+    src = "".join(open(os.path.join(PKG, "csrc", f)).read() for f in (
+        "crc32c_device.hip", "crc32c_fold.inc", "crc32c_wide.inc", "crc32c_narrow.inc", "crc32c_support.inc"))
     for switch in ("kAbl", "kStrided", "kVIn", "c->variant", "c->narrow"):
         assert switch not in src, switch
     diag = open(os.path.join(PKG, "csrc", "crc32c_diag.inc")).read()
