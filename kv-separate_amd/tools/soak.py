@@ -45,6 +45,12 @@ def lengths(rng, n, kind):
     return ln
 
 
+def bad_rate(rng):
+    """Fraction of planted mismatches in a verify case: none, a few, 1 %, a third, or every block (round 5: the verify
+    form posts one verdict per workgroup, so the all-bad batch is its own path)."""
+    return float(rng.choice([0.0, 1e-4, 0.01, 0.33, 1.01], p=[0.15, 0.2, 0.35, 0.15, 0.15]))
+
+
 class Mismatch(AssertionError):
     pass
 
@@ -122,7 +128,7 @@ def soak(seed, seconds=None, max_cases=None, log=print, pool=POOL):
                           & np.uint64(0xFFFFFFFF))
                 for k in range(4):
                     img[(pos + ln + np.uint64(1 + k)).astype(np.int64)] = ((stored >> np.uint64(8 * k)) & 0xFF).astype(np.uint8)
-                bad = rng.random(n) < 0.01
+                bad = rng.random(n) < bad_rate(rng)
                 img[(pos[bad] + ln[bad] + np.uint64(1)).astype(np.int64)] ^= np.uint8(1)
                 d_img = torch.from_numpy(img).to(dev)
                 tw = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -165,7 +171,7 @@ def soak(seed, seconds=None, max_cases=None, log=print, pool=POOL):
             continue
         if verify:
             masked = np.array([kvsep.mask(int(x)) for x in exp], dtype=np.uint32)
-            bad = rng.random(n) < 0.01
+            bad = rng.random(n) < bad_rate(rng)
             masked[bad] ^= np.uint32(1 << int(rng.integers(0, 32)))
             fb = torch.zeros(1, dtype=torch.int64, device=dev)
             nb = torch.zeros(1, dtype=torch.int64, device=dev)
