@@ -520,6 +520,33 @@ def launch_ranks(n: int) -> int:
     return worst
 
 
+def line_failures(line: dict, world: int, same_device: bool) -> list:
+    """Why a printed line is not a clean measurement: bench.py prints the line and then exits
+    non-zero when any of these holds, so a driver that takes its rc and value from this process never records a
+    wrong-result or mis-placed run as clean.  A checksum mismatch is Corruption in the reference
+    (/root/reference/db/value_log_reader.cc:112-122), never a number."""
+    bad = []
+    parity = line.get("parity")
+    if parity is not None and not parity.get("all_blocks_match"):
+        bad.append(f"parity: {parity.get('mismatches')} mismatching blocks, "
+                   f"{parity.get('mismatching_digest_ranges')} mismatching digest ranges")
+    verdict = line.get("verify")
+    if verdict is not None and not verdict.get("ok"):
+        bad.append(f"verify: first_bad {verdict.get('first_bad')} nbad {verdict.get('nbad')}, expected "
+                   f"{verdict.get('expected_first_bad')} / {verdict.get('expected_nbad')}")
+    if line.get("host_roundtrip_parity") is False:
+        bad.append("host round trip: results differ from the device-resident run")
+    per_rank = line.get("per_rank") or []
+    got = sorted(r.get("rank") for r in per_rank if isinstance(r, dict) and r.get("rank") is not None)
+    if got != list(range(world)):
+        bad.append(f"per-rank records: got ranks {got} of {world}")
+    summary = line.get("per_rank_summary") or {}
+    if world > 1 and not same_device and not summary.get("distinct_devices"):
+        bad.append(f"{world} ranks but not on distinct devices (PCI bus IDs {summary.get('pci_bus_ids')}); a "
+                   f"same-device rehearsal sets KVSEP_BENCH_SAME_DEVICE")
+    return bad
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -586,13 +613,23 @@ def main():
         t_start = time.time()
         rec = rank_record(rank, local, None, {"numa_node": None, "bound_cpus": 0}, None, 1.0, t_start, time.time(),
                           GIB, None)
+        ids = os.environ.get("KVSEP_BENCH_DRYRUN_BUS_IDS")  # launcher test: the bus ID each rank's GPU would report
+        if ids:
+            rec["pci_bus_id"] = (ids.split(",") + [None] * world)[rank]
         per_rank = shard.gather_objects(rec, dist if world > 1 else None)
+        failures = []
         if rank == 0:
-            print(json.dumps({"dry_run": True, "n_gpus": world, "world_size": world,
-                              "backend": dist.get_backend() if world > 1 else None, "per_rank": per_rank,
-                              "per_rank_summary": shard.rank_summary(per_rank, same_device=False)}), flush=True)
+            same = bool(os.environ.get("KVSEP_BENCH_SAME_DEVICE"))
+            line = {"dry_run": True, "n_gpus": world, "world_size": world,
+                    "backend": dist.get_backend() if world > 1 else None, "per_rank": per_rank,
+                    "per_rank_summary": shard.rank_summary(per_rank, same_device=same)}
+            failures = line["failures"] = line_failures(line, world, same)
+            print(json.dumps(line), flush=True)
         if world > 1:
             dist.destroy_process_group()
+        if failures:
+            log(f"[rank 0] the line above is not a clean measurement: {'; '.join(failures)}")
+            sys.exit(1)
         return
     # Started by a launcher (torchrun, launch_ranks): a process group, RCCL with one rank per GPU -- also at one rank,
     # so `torchrun --nproc-per-node 1 bench.py` runs the same RCCL init and collectives as eight ranks do
@@ -792,6 +829,9 @@ def main():
                    "reduction": "all-reduce MIN of first_bad (global index) and SUM of nbad over the ranks"
                    if dd else "one rank"}
     crcs = out[:, :count].cpu().numpy().view(np.uint32).reshape(-1)
+    if os.environ.get("KVSEP_BENCH_CORRUPT_RESULT") == str(rank) and crcs.size:  # test hook: one wrong gathered word
+        crcs = crcs.copy()
+        crcs[crcs.size // 2] ^= np.uint32(1)
     results = shard.gather_results(crcs, dd, coll_dev)
     digests = [shard.crc_of_crcs(r, kvsep.extend_host) for r in results]
 
@@ -1001,10 +1041,15 @@ def main():
             "form": args.form,
             "verify": verdict,
         }
+        failures = line_failures(line, world, same_device)
+        line["failures"] = failures
         print(json.dumps(line), flush=True)
     ctx.close()
     if dd:
         dist.destroy_process_group()
+    if rank == 0 and failures:
+        log(f"[rank 0] the line above is not a clean measurement: {'; '.join(failures)}")
+        sys.exit(1)
 
 
 if __name__ == "__main__":

@@ -32,9 +32,12 @@ extern "C" {
  * rebuilt; check kvsep_abi_version() == KVSEP_ABI_VERSION once at startup.  3 (round 5): kvsep_offload_stats counts
  * only calls at or above the offload threshold (since round 4: host_calls no longer includes the calls below it, which
  * are not counted at all); new entry points for the host legs, topology and host placement; no signature changed.
+ * 4 (round 6): graph captures get capture sets of their own (kvsep_crc32c_reserve_captures / _release_captures /
+ * _capture_sets); the fault-injection hook left this header (csrc/kvsep_testing.h) and works only under
+ * KVSEP_TEST_HOOKS=1; no signature changed.
  * The reference's C++ symbol leveldb::crc32c::Extend is not in this library: it is in the libkvsep_leveldb_abi.so
  * shim. */
-#define KVSEP_ABI_VERSION 3
+#define KVSEP_ABI_VERSION 4
 int kvsep_abi_version(void);
 
 #define KVSEP_OK 0
@@ -101,13 +104,25 @@ int kvsep_crc32c_ctx_set_host_node(kvsep_crc32c_ctx* ctx, int node);
  * holding its first pinned staging slot (-1: not allocated yet / unknown), cpus[0..cap) = the CPUs its copier threads
  * are bound to.  Returns the number of those CPUs (0: not bound), or KVSEP_EINVAL. */
 int kvsep_crc32c_ctx_host_placement(kvsep_crc32c_ctx* ctx, int* device_node, int* staging_node, int* cpus, int cap);
-/* Fault injection (tests): the context's next batched call returns KVSEP_EHIP right after it enqueued its CRC kernel,
- * before the combine kernel of a planned batch -- the one point where a verify call's accumulators hold posts that no
- * kernel will publish.  The next verify call on the context resets them first, so its verdict is exact. */
-int kvsep_crc32c_ctx_inject_failure(kvsep_crc32c_ctx* ctx);
-/* Pre-size scratch so later calls of up to `count` blocks / `total_bytes` bytes do not allocate
- * (required before graph capture; covers the planned, narrow, verify and SST-verify forms). */
+/* Pre-size scratch so later calls of up to `count` blocks / `total_bytes` bytes do not allocate: the context's own
+ * scratch (eager calls) and every free capture set (at least 4 are made).  Required before graph capture; covers the
+ * planned, narrow, verify and SST-verify forms. */
 int kvsep_crc32c_reserve(kvsep_crc32c_ctx* ctx, uint64_t count, uint64_t total_bytes);
+/* Graph capture (hipStreamBeginCapture ... EndCapture, torch.cuda.graph): every call captured into one graph runs on
+ * that capture's own capture set -- its piece plan, work counter, SST arrays and verify verdict slots -- held by it until
+ * kvsep_crc32c_release_captures.  So graphs of one context may be replayed at the same time on different streams, and
+ * a verify graph replayed over itself (two streams, two instantiations) writes identical verdicts.  The calls of ONE
+ * graph share its set and must be ordered inside the graph (captured on one stream, or joined); a graph holding
+ * planned batches (max_len 0 or above the piece size) must not overlap a replay of itself.  A capture that finds no free
+ * set fails with KVSEP_EINVAL when its first call is captured.
+ * reserve_captures: at least nsets sets, free ones sized by the largest kvsep_crc32c_reserve so far (held sets keep the
+ *   size their graph captured).
+ * release_captures: every set free again -- call it only once the graphs captured so far are destroyed (a later
+ *   reserve may reallocate a free set).
+ * capture_sets: returns the number of sets; *held (nullable) = how many a graph holds. */
+int kvsep_crc32c_reserve_captures(kvsep_crc32c_ctx* ctx, int nsets);
+int kvsep_crc32c_release_captures(kvsep_crc32c_ctx* ctx);
+int kvsep_crc32c_capture_sets(kvsep_crc32c_ctx* ctx, int* held);
 /* Kernel timing with HIP events on the caller's stream, around the main CRC kernel only. */
 int kvsep_crc32c_ctx_set_timing(kvsep_crc32c_ctx* ctx, int enable);
 int kvsep_crc32c_ctx_get_timing(kvsep_crc32c_ctx* ctx, double* total_ms, uint64_t* launches); /* syncs + resets */

@@ -34,12 +34,14 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
 
 #include "../../include/kvsep_crc32c.h"
 #include "gf2.h"
+#include "kvsep_testing.h"
 #include "kvsep_internal.h"
 
 namespace kvsep {
@@ -55,6 +57,18 @@ namespace kvsep {
 // host side
 using namespace kvsep;
 
+// A graph capture's own scratch (round 6).  Every call captured into one graph -- one capture
+// sequence, hipStreamGetCaptureInfo's id -- runs on the same capture set, and no other capture shares it while it is
+// held, so two graphs replayed at once never share a plan, a work counter, SST arrays or verdict slots, and replays of
+// one graph write identical words.  Sets are sized by kvsep_crc32c_reserve before capture (nothing is allocated under
+// capture) and stay held, frozen in size, until kvsep_crc32c_release_captures: a graph keeps the pointers it captured.
+struct CaptureSet {
+  unsigned long long id = 0;
+  bool held = false;
+  Scratch sc;
+};
+constexpr size_t kDefaultCaptureSets = 4;
+
 struct kvsep_crc32c_ctx {
   int device = 0;
   int num_cus = 0;
@@ -65,6 +79,8 @@ struct kvsep_crc32c_ctx {
   int kernel = 0;    // kvsep_crc32c_ctx_set_kernel: 0 auto (use_narrow), 1 wide only, 2-6 narrow when the hint allows
   uint32_t static_contig = 1;  // static schedule: contiguous runs (1) or round-robin items (0, set_schedule(2))
   Scratch sc;  // scratch of the calls made directly on this context (any stream, event-ordered)
+  std::vector<std::unique_ptr<CaptureSet>> caps;  // scratch of captured calls, one set per graph capture
+  uint64_t res_count = 0, res_bytes = 0;          // the largest reservation: what capture sets are sized for
   int host_node = -1;        // NUMA node of the device's PCI function (-1: unknown / not bound): host legs go there
   bool inject_failure = false;  // kvsep_crc32c_ctx_inject_failure: the next call fails right after its CRC kernel
   // timing
@@ -145,43 +161,56 @@ int release(Scratch& sc, hipStream_t s) {
   return KVSEP_OK;
 }
 
-// The verify form's device words (allocated once per scratch, before any capture -- kvsep_crc32c_reserve does it): on
-// the first 128-B line the result words of a call whose caller passes none; then kVaccLines sets of the accumulators
-// the kernels post to and reset (PiecesArgs::vacc: the lowest-block word and the final arrival word, then 8 shard
-// arrival words, each group on a line of its own), which must start in their reset state: ~0 (no mismatch), 0
-// (nothing arrived, none bad).  Set 0 serves eager calls, which the scratch's events order one after another; each
-// captured call takes one of the other sets in turn, so replays of up to kVaccLines - 1 captured verify calls may
-// overlap (two graphs on two streams) without mixing their arrivals.
-constexpr uint32_t kVaccLines = 8, kVaccSetWords = kVaccStride * (1 + kVaccShards);
-unsigned long long* vacc_set(Scratch& sc, uint32_t line) { return sc.d_verify + kVaccStride + line * kVaccSetWords; }
+// The verify form's device words (allocated once per scratch -- kvsep_crc32c_reserve does it for capture sets): on the
+// first 128-B line the result words of a call whose caller passes none; then the accumulators eager calls post to and
+// reset (PiecesArgs::vacc: the lowest-block word and the final arrival word, then 8 shard arrival words, each group on
+// a line of its own), which must start in their reset state: ~0 (no mismatch), 0 (nothing arrived, none bad).  Eager
+// calls on one scratch are ordered one after another by its events, so one set serves them all; captured calls publish
+// through verdict slots instead (ensure_vslot), which hold no state from one call to the next.
+constexpr uint32_t kVaccSetWords = kVaccStride * (1 + kVaccShards);
+unsigned long long* vacc_set(Scratch& sc) { return sc.d_verify + kVaccStride; }
 
 int ensure_verify(Scratch& sc) {
   if (sc.d_verify) return KVSEP_OK;
-  std::vector<unsigned long long> init(kVaccStride + kVaccLines * kVaccSetWords, 0ull);
-  init[0] = ~0ull;  // default first_bad
-  for (uint32_t l = 0; l < kVaccLines; ++l) init[kVaccStride + l * kVaccSetWords] = ~0ull;  // each set's vacc[0]
+  std::vector<unsigned long long> init(kVaccStride + kVaccSetWords, 0ull);
+  init[0] = ~0ull;             // default first_bad
+  init[kVaccStride] = ~0ull;   // the set's vacc[0]
   KVSEP_HIP(hipMalloc(&sc.d_verify, init.size() * 8));
   KVSEP_HIP(hipMemcpy(sc.d_verify, init.data(), init.size() * 8, hipMemcpyHostToDevice));
-  sc.vacc_dirty = 0;
+  sc.vacc_dirty = false;
   return KVSEP_OK;
 }
 
-// Puts accumulator set `line` back in its reset state, in stream order (capturable: two memsets).  Needed after a call
+// Verdict slots of captured verify calls: one per workgroup of the CRC kernel (num_cus) and of the combine kernel.
+uint32_t vslots_needed(const kvsep_crc32c_ctx* c) { return uint32_t(c->num_cus) + kCombineMaxGrid; }
+
+int ensure_vslot(Scratch& sc, uint32_t n) {
+  if (sc.cap_vslot >= n) return KVSEP_OK;
+  hipFree(sc.d_vslot);
+  sc.d_vslot = nullptr;
+  sc.cap_vslot = 0;
+  KVSEP_HIP(hipMalloc(&sc.d_vslot, uint64_t(n) * 16));
+  sc.cap_vslot = n;
+  return KVSEP_OK;
+}
+
+// Puts the eager accumulator set back in its reset state, in stream order (two memsets).  Needed after an eager call
 // that failed once its CRC kernel was enqueued: the kernel's posts stay in the set, and with no publishing kernel after
-// them nothing resets it -- the next verdict would inherit a stale count and first_bad.  Under capture the
-// memsets only become graph nodes that may never run, so the set stays marked (every later captured call on it resets
-// it first, at the cost of two memset nodes) until an eager call has reset it.
-int reset_vacc(Scratch& sc, uint32_t line, hipStream_t s, bool capturing) {
-  unsigned long long* v = vacc_set(sc, line);
+// them nothing resets it -- the next verdict would inherit a stale count and first_bad.  The failed call
+// marks the set (vacc_dirty) and the next eager verify call on the scratch resets it first.  Captured calls never need
+// this: their slots are overwritten whole by every replay.
+int reset_vacc(Scratch& sc, hipStream_t s) {
+  unsigned long long* v = vacc_set(sc);
   KVSEP_HIP(hipMemsetAsync(v, 0, kVaccSetWords * 8, s));
   KVSEP_HIP(hipMemsetAsync(v, 0xff, 8, s));
-  if (!capturing) sc.vacc_dirty &= ~(1u << line);
+  sc.vacc_dirty = false;
   return KVSEP_OK;
 }
 
 // SST verify scratch (len + 1 and the stored trailer words per block).
-int ensure_sst(Scratch& sc, uint64_t count) {
+int ensure_sst(Scratch& sc, uint64_t count, bool capturing = false) {
   if (count <= sc.cap_sst) return KVSEP_OK;
+  if (capturing) return set_err(KVSEP_EINVAL, "SST verify under capture needs kvsep_crc32c_reserve first");
   int rc = quiesce(sc);
   if (rc) return rc;
   hipFree(sc.d_sst_len1);
@@ -195,12 +224,14 @@ int ensure_sst(Scratch& sc, uint64_t count) {
   return KVSEP_OK;
 }
 
-int ensure_plan(Scratch& sc, uint64_t piece_bytes, uint64_t count, uint64_t total_bytes) {
+int ensure_plan(Scratch& sc, uint64_t piece_bytes, uint64_t count, uint64_t total_bytes, bool capturing = false) {
   const uint64_t pieces = count + total_bytes / piece_bytes + 1;
   // hipcub's scan takes an int item count; piece and block indices are u32 in the kernels
   if (count > 0x7fffffffull) return set_err(KVSEP_EINVAL, "more than 2^31 - 1 blocks in one batch that needs a plan");
   if (pieces > 0xffffffffull) return set_err(KVSEP_EINVAL, "batch too large for u32 piece indices");
   if (count <= sc.cap_count && pieces <= sc.cap_pieces) return KVSEP_OK;
+  if (capturing)
+    return set_err(KVSEP_EINVAL, "a captured planned batch larger than kvsep_crc32c_reserve sized its capture set for");
   const uint64_t nc = std::max<uint64_t>(count, sc.cap_count), np = std::max<uint64_t>(pieces, sc.cap_pieces);
   int rc = quiesce(sc);
   if (rc) return rc;
@@ -275,6 +306,14 @@ int narrow_form(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes,
   const bool eight_waves = max_len <= 8 * 1024 ? count >= (1u << 17) : count >= (1u << 15);
   return eight_waves ? 9 : 6;
 }
+
+// The claim kernel's shipped levers (crc32c_narrow_claim_kernel's kLean, round 6): the fill fetching each table entry
+// once and no head / tail loads for groups without such chunks -- 16 of config 2's 52 non-payload loads per wave.  On
+// one MI355X, interleaved in one process against the round-5 form (diag variant 65; tools/narrow_variants_probe.py,
+// profiles/round6/claim_lean.log): 4 KiB blocks 128 MiB 24.66 vs 24.88 us, 256 MiB 43.93 vs 44.32, 1 GiB 153.98 vs
+// 154.06 -- about 1 % at config 2, the time the loads cost; the rest of config 2's distance to the streaming read is not
+// in instruction count.  Bit 2 (no init load for init-less batches) measured nothing and is not shipped.
+constexpr uint32_t kClaimLean = 3;
 
 bool use_narrow(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes, uint64_t max_len) {
   if (max_len == 0 || max_len > 2 * kNarrowMax) return false;
@@ -354,8 +393,36 @@ int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, bool captur
                     uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count, uint64_t total_bytes,
                     uint64_t max_len);
 
+// Is `s` capturing, and if so which capture set do its calls run on: the one this capture already holds, else the first
+// free one.  No free set is an error at capture time (KVSEP_EINVAL), never a shared set.
+int stream_scratch(kvsep_crc32c_ctx* c, hipStream_t s, Scratch& eager, bool* capturing, Scratch** out) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  KVSEP_HIP(hipStreamGetCaptureInfo(s, &cap, &id));
+  *capturing = cap != hipStreamCaptureStatusNone;
+  *out = &eager;
+  if (!*capturing) return KVSEP_OK;
+  for (auto& k : c->caps)
+    if (k->held && k->id == id) {
+      *out = &k->sc;
+      return KVSEP_OK;
+    }
+  for (auto& k : c->caps)
+    if (!k->held) {
+      k->held = true;
+      k->id = id;
+      *out = &k->sc;
+      return KVSEP_OK;
+    }
+  return set_err(KVSEP_EINVAL, c->caps.empty()
+                                   ? "graph capture needs kvsep_crc32c_reserve first (it sizes the capture sets)"
+                                   : "every capture set of this context is held by an earlier graph: "
+                                     "kvsep_crc32c_reserve_captures for more, or kvsep_crc32c_release_captures once "
+                                     "those graphs are destroyed");
+}
+
 // Every use of a Scratch is bracketed by acquire/release (event ordering across streams).
-int launch_batch(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* base, const uint64_t* off,
+int launch_batch(kvsep_crc32c_ctx* c, Scratch& eager, hipStream_t s, const void* base, const uint64_t* off,
                  const uint64_t* len, const uint32_t* init, const uint32_t* expect, uint32_t* out, uint64_t* first_bad,
                  uint64_t* nbad, uint64_t count, uint64_t total_bytes, uint64_t max_len) {
   if (!base || !off || !len || !out) return set_err(KVSEP_EINVAL, "null pointer argument");
@@ -363,14 +430,16 @@ int launch_batch(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* ba
   if (count > 0xffffffffull) return set_err(KVSEP_EINVAL, "more than 2^32 - 1 blocks in one batch");
   DeviceGuard dg(c->device);
   KVSEP_HIP(dg.err);
-  // Under stream capture (hipGraph) the call only records its nodes: the cross-stream scratch events are
-  // skipped (a captured wait on an event recorded outside the capture is not allowed), so the graph's user
-  // orders its replays against other uses of this context's scratch.  Allocation must not happen either:
-  // kvsep_crc32c_reserve first.
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  KVSEP_HIP(hipStreamIsCapturing(s, &cap));
-  const bool capturing = cap != hipStreamCaptureStatusNone;
-  int rc = capturing ? KVSEP_OK : acquire(sc, s);
+  // Under stream capture (hipGraph) the call only records its nodes, on its capture's own set (stream_scratch): the
+  // cross-stream scratch events are skipped (a captured wait on an event recorded outside the capture is not allowed)
+  // and nothing is allocated -- kvsep_crc32c_reserve sized the set.  Calls captured into one graph share its set, so
+  // they must be ordered within the graph (captured on one stream, or joined).
+  bool capturing = false;
+  Scratch* psc = nullptr;
+  int rc = stream_scratch(c, s, eager, &capturing, &psc);
+  if (rc) return rc;
+  Scratch& sc = *psc;
+  rc = capturing ? KVSEP_OK : acquire(sc, s);
   if (rc) return rc;
   rc = launch_batch_in(c, sc, s, capturing, base, off, len, init, expect, out, first_bad, nbad, count, total_bytes,
                        max_len);
@@ -381,37 +450,41 @@ int launch_batch(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, const void* ba
   return capturing ? KVSEP_OK : release(sc, s);
 }
 
-int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, PiecesArgs& a, const void* base,
-                      const uint64_t* off, const uint64_t* len, const uint32_t* init, const uint32_t* expect,
-                      uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count, uint64_t total_bytes,
-                      uint64_t max_len);
+int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, bool capturing, PiecesArgs& a,
+                      const void* base, const uint64_t* off, const uint64_t* len, const uint32_t* init,
+                      const uint32_t* expect, uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count,
+                      uint64_t total_bytes, uint64_t max_len);
 
 int launch_batch_in(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, bool capturing, const void* base,
                     const uint64_t* off, const uint64_t* len, const uint32_t* init, const uint32_t* expect,
                     uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count, uint64_t total_bytes,
                     uint64_t max_len) {
   PiecesArgs a{};
-  uint32_t line = 0;
   if (expect) {
-    int rc = ensure_verify(sc);
-    if (rc) return rc;
-    line = capturing ? 1 + (sc.vacc_next++ % (kVaccLines - 1)) : 0;
-    if (sc.vacc_dirty & (1u << line)) {
-      rc = reset_vacc(sc, line, s, capturing);
+    if (capturing) {  // verdict slots (reserved with the capture set), published by the reduce kernel
+      if (!sc.d_verify || sc.cap_vslot < vslots_needed(c))
+        return set_err(KVSEP_EINVAL, "verify under capture needs kvsep_crc32c_reserve first");
+      a.vslot = sc.d_vslot;
+    } else {
+      int rc = ensure_verify(sc);
       if (rc) return rc;
+      if (sc.vacc_dirty) {
+        rc = reset_vacc(sc, s);
+        if (rc) return rc;
+      }
+      a.vacc = vacc_set(sc);  // the accumulators, in their reset state: the kernels publish the verdict
     }
-    a.vacc = vacc_set(sc, line);  // the accumulators, in their reset state: the kernels publish the verdict
   }
-  const int rc = launch_batch_body(c, sc, s, a, base, off, len, init, expect, out, first_bad, nbad, count, total_bytes,
-                                   max_len);
-  if (rc && expect) sc.vacc_dirty |= 1u << line;  // a kernel may have posted to the set: reset it before its next use
+  const int rc = launch_batch_body(c, sc, s, capturing, a, base, off, len, init, expect, out, first_bad, nbad, count,
+                                   total_bytes, max_len);
+  if (rc && expect && !capturing) sc.vacc_dirty = true;  // a kernel may have posted to the set: reset it first next time
   return rc;
 }
 
-int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, PiecesArgs& a, const void* base,
-                      const uint64_t* off, const uint64_t* len, const uint32_t* init, const uint32_t* expect,
-                      uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count, uint64_t total_bytes,
-                      uint64_t max_len) {
+int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, bool capturing, PiecesArgs& a,
+                      const void* base, const uint64_t* off, const uint64_t* len, const uint32_t* init,
+                      const uint32_t* expect, uint32_t* out, uint64_t* first_bad, uint64_t* nbad, uint64_t count,
+                      uint64_t total_bytes, uint64_t max_len) {
   const bool planned = !(max_len != 0 && max_len <= c->piece_bytes);
   a.base = static_cast<const uint8_t*>(base);
   a.off = off;
@@ -426,9 +499,10 @@ int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, PiecesArg
       first_bad = reinterpret_cast<uint64_t*>(sc.d_verify);
       nbad = reinterpret_cast<uint64_t*>(sc.d_verify + 1);
     }
-    if (count == 0) {          // nothing to check, no kernel: the verdict is "none" (first_bad = ~0, nbad = 0)
-      KVSEP_HIP(hipMemsetAsync(first_bad, 0xff, 8, s));
-      KVSEP_HIP(hipMemsetAsync(nbad, 0, 8, s));
+    if (count == 0) {  // nothing to check, no CRC kernel: the verdict is "none" (first_bad = ~0, nbad = 0)
+      start_words_kernel<<<1, 64, 0, s>>>(nullptr, reinterpret_cast<unsigned long long*>(first_bad),
+                                          reinterpret_cast<unsigned long long*>(nbad));
+      KVSEP_HIP(hipGetLastError());
     }
   }
   a.expect = expect;
@@ -438,24 +512,6 @@ int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, PiecesArg
   // the A/B variants of the KVSEP_DIAG tools build fall back to the separate verify_finish_kernel pass.
   bool fused = true;
   if (count == 0) return KVSEP_OK;
-  if (planned) {
-    int rc = ensure_plan(sc, a.piece_bytes, count, total_bytes);
-    if (rc) return rc;
-    a.pstart = sc.d_pstart;
-    a.pblk = sc.d_pblk;
-    a.partial = sc.d_partial;
-    a.max_pieces = sc.cap_pieces;
-    const unsigned nb = unsigned((count + 255) / 256);
-    crc32c_plan_count_kernel<<<nb, 256, 0, s>>>(len, count, a.piece_bytes, sc.d_counts);
-    KVSEP_HIP(hipGetLastError());
-    KVSEP_HIP(hipMemsetAsync(sc.d_pstart, 0, 8, s));
-    size_t tb = sc.scan_tmp_bytes;
-    KVSEP_HIP(hipcub::DeviceScan::InclusiveSum(sc.d_scan_tmp, tb, sc.d_counts, sc.d_pstart + 1, int(count), s));
-    crc32c_plan_expand_kernel<<<nb, 256, 0, s>>>(sc.d_pstart, count, sc.cap_pieces, sc.d_pblk);
-    KVSEP_HIP(hipGetLastError());
-  } else {
-    a.max_pieces = count;
-  }
   // auto schedule: guided (one atomic per grab) for planned batches with many pieces; static for the rest --
   // a few thousand small pieces would spend most of the kernel in single-item grabs on one counter
   // (~88 dequeues/us, MI355X_MICROARCH.md dequeue)
@@ -466,9 +522,33 @@ int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, PiecesArg
   a.guided_div = 0;  // adaptive (crc32c_pieces_kernel)
   a.guided_cap = 0;
   if (dyn) {
+    if (!sc.d_counter && capturing) return set_err(KVSEP_EINVAL, "graph capture needs kvsep_crc32c_reserve first");
     if (!sc.d_counter) KVSEP_HIP(hipMalloc(&sc.d_counter, 16));
     a.work_counter = sc.d_counter;
-    KVSEP_HIP(hipMemsetAsync(sc.d_counter, 0, 4, s));
+  }
+  // The start-state words (pstart[0], the guided counter) are written by a kernel of the call, never by a memset node
+  // (see crc32c_plan_count_kernel).
+  if (planned) {
+    int rc = ensure_plan(sc, a.piece_bytes, count, total_bytes, capturing);
+    if (rc) return rc;
+    a.pstart = sc.d_pstart;
+    a.pblk = sc.d_pblk;
+    a.partial = sc.d_partial;
+    a.max_pieces = sc.cap_pieces;
+    const unsigned nb = unsigned((count + 255) / 256);
+    crc32c_plan_count_kernel<<<nb, 256, 0, s>>>(len, count, a.piece_bytes, sc.d_counts, sc.d_pstart,
+                                                dyn ? sc.d_counter : nullptr);
+    KVSEP_HIP(hipGetLastError());
+    size_t tb = sc.scan_tmp_bytes;
+    KVSEP_HIP(hipcub::DeviceScan::InclusiveSum(sc.d_scan_tmp, tb, sc.d_counts, sc.d_pstart + 1, int(count), s));
+    crc32c_plan_expand_kernel<<<nb, 256, 0, s>>>(sc.d_pstart, count, sc.cap_pieces, sc.d_pblk);
+    KVSEP_HIP(hipGetLastError());
+  } else {
+    a.max_pieces = count;
+    if (dyn) {
+      start_words_kernel<<<1, 64, 0, s>>>(sc.d_counter, nullptr, nullptr);
+      KVSEP_HIP(hipGetLastError());
+    }
   }
   const unsigned grid = unsigned(c->num_cus);  // one workgroup per CU, persistent
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -484,7 +564,7 @@ int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, PiecesArg
     if (expect && (nv == 6 || nv == 9 || nv == 10 || nv == 11 || nv == 20)) {  // verify form of the shipped forms
       switch (nv) {
         case 9: crc32c_narrow_kernel<4, true, 512, true, true, LdsFull, true><<<grid, 512, 0, s>>>(a); break;
-        case 10: crc32c_narrow_claim_kernel<4, 512, true><<<grid, 512, 0, s>>>(a); break;
+        case 10: crc32c_narrow_claim_kernel<4, 512, true, true, 8, kClaimLean><<<grid, 512, 0, s>>>(a); break;
         case 11: crc32c_narrow_claim_kernel<4, 512, true, true, 16><<<grid, 512, 0, s>>>(a); break;
         case 20: crc32c_narrow_sorted_kernel<4, true, 1024, true><<<grid, 1024, 0, s>>>(a); break;
         default: crc32c_narrow_kernel<4, true, 1024, false, true, LdsFull, true><<<grid, 1024, 0, s>>>(a); break;
@@ -496,11 +576,12 @@ int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, PiecesArg
       KVSEP_HIP(hipMemsetAsync(first_bad, 0xff, 8, s));
       KVSEP_HIP(hipMemsetAsync(nbad, 0, 8, s));
     }
+    a.vslot = nullptr;  // (their compare posts to the caller's words, captured or not)
     fused = !expect || diag_self_compare(nv);
     if (!diag_launch_narrow(nv, grid, s, a, count))  // KVSEP_DIAG build only
     switch (nv) {
       case 9: crc32c_narrow_kernel<4, true, 512, true><<<grid, 512, 0, s>>>(a); break;
-      case 10: crc32c_narrow_claim_kernel<4, 512><<<grid, 512, 0, s>>>(a); break;
+      case 10: crc32c_narrow_claim_kernel<4, 512, false, true, 8, kClaimLean><<<grid, 512, 0, s>>>(a); break;
       case 11: crc32c_narrow_claim_kernel<4, 512, false, true, 16><<<grid, 512, 0, s>>>(a); break;
       case 20: crc32c_narrow_sorted_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
       default: crc32c_narrow_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
@@ -518,9 +599,17 @@ int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, PiecesArg
     KVSEP_HIP(hipEventRecord(e1, s));
     c->ev_pending.emplace_back(e0, e1);
   }
+  const unsigned cgrid = unsigned(std::min<uint64_t>((count + 255) / 256, kCombineMaxGrid));
   if (planned) {
-    if (expect) crc32c_combine_kernel<true><<<unsigned((count + 255) / 256), 256, 0, s>>>(a);
-    else crc32c_combine_kernel<false><<<unsigned((count + 255) / 256), 256, 0, s>>>(a);
+    a.vslot_base = grid;  // a captured verify call: the combine kernel's slots follow the CRC kernel's
+    if (expect) crc32c_combine_kernel<true><<<cgrid, 256, 0, s>>>(a);
+    else crc32c_combine_kernel<false><<<cgrid, 256, 0, s>>>(a);
+    KVSEP_HIP(hipGetLastError());
+  }
+  if (expect && fused && a.vslot) {  // a captured verify call's verdict from its slots
+    verify_slots_reduce_kernel<<<1, 256, 0, s>>>(a.vslot, grid + (planned ? cgrid : 0u),
+                                                 reinterpret_cast<unsigned long long*>(first_bad),
+                                                 reinterpret_cast<unsigned long long*>(nbad));
     KVSEP_HIP(hipGetLastError());
   }
   if (expect && !fused) {
@@ -544,6 +633,7 @@ void free_scratch(Scratch& sc) {
   free_plan(sc);
   hipFree(sc.d_counter);
   hipFree(sc.d_verify);
+  hipFree(sc.d_vslot);
   hipFree(sc.d_sst_len1);
   hipFree(sc.d_sst_stored);
   if (sc.last_use) (void)hipEventDestroy(sc.last_use);
@@ -598,6 +688,7 @@ void kvsep_crc32c_ctx_destroy(kvsep_crc32c_ctx* c) {
   DeviceGuard dg(c->device);
   hipDeviceSynchronize();
   free_scratch(c->sc);
+  for (auto& k : c->caps) free_scratch(k->sc);
   hipFree(c->d_tabs);
   for (auto& p : c->ev_pending) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
   for (auto e : c->ev_pool) hipEventDestroy(e);
@@ -609,6 +700,9 @@ void kvsep_crc32c_ctx_destroy(kvsep_crc32c_ctx* c) {
 int kvsep_crc32c_ctx_set_piece_bytes(kvsep_crc32c_ctx* c, uint64_t piece_bytes) {
   if (!c || piece_bytes < 1024 || piece_bytes % 1024) return set_err(KVSEP_EINVAL, "piece_bytes must be a multiple of 1 KiB");
   std::lock_guard<std::mutex> g(c->mu);
+  // a captured graph holds this piece size and the table image it reads (Z_piece): it would replay wrong
+  for (auto& k : c->caps)
+    if (k->held) return set_err(KVSEP_EINVAL, "set_piece_bytes with captured graphs held: kvsep_crc32c_release_captures first");
   DeviceGuard dg(c->device);
   KVSEP_HIP(dg.err);
   KVSEP_HIP(hipDeviceSynchronize());
@@ -616,6 +710,7 @@ int kvsep_crc32c_ctx_set_piece_bytes(kvsep_crc32c_ctx* c, uint64_t piece_bytes) 
   c->piece_auto = false;
   free_plan(c->sc);  // piece tables depend on piece_bytes (device already idle)
   for (auto& sc : c->staging.scratch) free_plan(sc);
+  for (auto& k : c->caps) free_plan(k->sc);  // none is held (above); kvsep_crc32c_reserve sizes them again
   return upload_tables(c);
 }
 
@@ -643,25 +738,82 @@ int kvsep_crc32c_ctx_set_host_node(kvsep_crc32c_ctx* c, int node) {
 
 int kvsep_crc32c_ctx_inject_failure(kvsep_crc32c_ctx* c) {
   if (!c) return set_err(KVSEP_EINVAL, "null ctx");
+  // a test hook (csrc/kvsep_testing.h, not the public header): inert unless the test environment asks for it
+  const char* on = std::getenv("KVSEP_TEST_HOOKS");
+  if (!on || std::strcmp(on, "1") != 0) return set_err(KVSEP_EINVAL, "fault injection needs KVSEP_TEST_HOOKS=1");
   std::lock_guard<std::mutex> g(c->mu);
   c->inject_failure = true;
   return KVSEP_OK;
 }
+
+}  // extern "C"
+
+namespace {
+// Everything a call of up to count blocks / total_bytes could allocate on this scratch.
+int reserve_scratch(kvsep_crc32c_ctx* c, Scratch& sc, uint64_t count, uint64_t total_bytes) {
+  if (!sc.d_counter) KVSEP_HIP(hipMalloc(&sc.d_counter, 16));
+  int rc = ensure_verify(sc);
+  if (rc) return rc;
+  if (!sc.last_use) KVSEP_HIP(hipEventCreateWithFlags(&sc.last_use, hipEventDisableTiming));
+  rc = ensure_sst(sc, count);
+  if (rc) return rc;
+  rc = ensure_vslot(sc, vslots_needed(c));
+  if (rc) return rc;
+  const uint32_t* zp = nullptr;
+  return ensure_plan(sc, piece_for(c, total_bytes, &zp), count, total_bytes);
+}
+
+// At least n capture sets, each free one sized for the context's largest reservation (held ones stay as their graph
+// captured them).
+int reserve_capture_sets(kvsep_crc32c_ctx* c, size_t n) {
+  while (c->caps.size() < n) c->caps.emplace_back(new CaptureSet());
+  for (auto& k : c->caps) {
+    if (k->held) continue;
+    int rc = reserve_scratch(c, k->sc, c->res_count, c->res_bytes);
+    if (rc) return rc;
+  }
+  return KVSEP_OK;
+}
+}  // namespace
+
+extern "C" {
 
 int kvsep_crc32c_reserve(kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes) {
   if (!c) return set_err(KVSEP_EINVAL, "null ctx");
   std::lock_guard<std::mutex> g(c->mu);
   DeviceGuard dg(c->device);
   KVSEP_HIP(dg.err);
-  // everything a later call could allocate, so that the call can be captured into a hipGraph
-  if (!c->sc.d_counter) KVSEP_HIP(hipMalloc(&c->sc.d_counter, 16));
-  int vr = ensure_verify(c->sc);
-  if (vr) return vr;
-  if (!c->sc.last_use) KVSEP_HIP(hipEventCreateWithFlags(&c->sc.last_use, hipEventDisableTiming));
-  int rc = ensure_sst(c->sc, count);
+  // everything a later call could allocate: on the context's own scratch (eager calls), and on every free capture set
+  // (the calls of a graph capture, which must not allocate)
+  int rc = reserve_scratch(c, c->sc, count, total_bytes);
   if (rc) return rc;
-  const uint32_t* zp = nullptr;
-  return ensure_plan(c->sc, piece_for(c, total_bytes, &zp), count, total_bytes);
+  c->res_count = std::max(c->res_count, count);
+  c->res_bytes = std::max(c->res_bytes, total_bytes);
+  return reserve_capture_sets(c, std::max(c->caps.size(), kDefaultCaptureSets));
+}
+
+int kvsep_crc32c_reserve_captures(kvsep_crc32c_ctx* c, int nsets) {
+  if (!c || nsets < 0 || nsets > 4096) return set_err(KVSEP_EINVAL, "nsets must be 0..4096");
+  std::lock_guard<std::mutex> g(c->mu);
+  DeviceGuard dg(c->device);
+  KVSEP_HIP(dg.err);
+  return reserve_capture_sets(c, size_t(nsets));
+}
+
+int kvsep_crc32c_release_captures(kvsep_crc32c_ctx* c) {
+  if (!c) return set_err(KVSEP_EINVAL, "null ctx");
+  std::lock_guard<std::mutex> g(c->mu);
+  for (auto& k : c->caps) k->held = false;
+  return KVSEP_OK;
+}
+
+int kvsep_crc32c_capture_sets(kvsep_crc32c_ctx* c, int* held) {
+  if (!c) return set_err(KVSEP_EINVAL, "null ctx");
+  std::lock_guard<std::mutex> g(c->mu);
+  int h = 0;
+  for (auto& k : c->caps) h += k->held ? 1 : 0;
+  if (held) *held = h;
+  return int(c->caps.size());
 }
 
 int kvsep_crc32c_ctx_set_timing(kvsep_crc32c_ctx* c, int enable) {
@@ -751,16 +903,16 @@ int kvsep_sst_verify_device(kvsep_crc32c_ctx* c, void* stream, const void* file_
   hipStream_t s = static_cast<hipStream_t>(stream);
   DeviceGuard dg(c->device);
   KVSEP_HIP(dg.err);
-  Scratch& sc = c->sc;
-  // as launch_batch: under capture no cross-stream events and no allocation (kvsep_crc32c_reserve sizes SST
-  // scratch too)
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  KVSEP_HIP(hipStreamIsCapturing(s, &cap));
-  const bool capturing = cap != hipStreamCaptureStatusNone;
-  if (capturing && count > sc.cap_sst) return set_err(KVSEP_EINVAL, "SST verify under capture needs kvsep_crc32c_reserve first");
-  int rc = capturing ? KVSEP_OK : acquire(sc, s);
+  // as launch_batch: under capture the capture's own set, no cross-stream events and no allocation
+  // (kvsep_crc32c_reserve sizes the SST arrays too)
+  bool capturing = false;
+  Scratch* psc = nullptr;
+  int rc = stream_scratch(c, s, c->sc, &capturing, &psc);
   if (rc) return rc;
-  rc = ensure_sst(sc, count);
+  Scratch& sc = *psc;
+  rc = capturing ? KVSEP_OK : acquire(sc, s);
+  if (rc) return rc;
+  rc = ensure_sst(sc, count, capturing);
   if (rc) return rc;
   if (count) {
     sst_verify_prep_kernel<<<unsigned((count + 255) / 256), 256, 0, s>>>(static_cast<const uint8_t*>(file_base), off,

@@ -488,7 +488,7 @@ int kvsep_abi_version(void) { return KVSEP_ABI_VERSION; }
 
 const char* kvsep_build_info(void) {
   return "kvsep_crc32c: gfx950 HIP kernels (LDS-replicated Z_1024 stride chains, v_perm addressing), "
-         "host legs: VPCLMULQDQ fold / SSE4.2 crc32 / portable slicing-by-8, ABI 3";
+         "host legs: VPCLMULQDQ fold / SSE4.2 crc32 / portable slicing-by-8, ABI 4";
 }
 
 const char* kvsep_crc32c_host_path(void) { return host_leg_name(host_leg()); }

@@ -26,21 +26,39 @@ struct kvsep_crc32c_group {
   std::vector<hipStream_t> stream;  // device-resident form: one stream per member, on its device
   std::vector<uint64_t*> d_res;      // verify form: [first_bad, nbad] of each member's shard, on its device
   std::mutex mu;                     // device-resident calls share the streams and d_res: one at a time
+  // each member's host node and its CPU list, read from sysfs once per node (not on every call)
+  std::mutex node_mu;
+  std::vector<int> node;
+  std::vector<std::vector<int>> node_cpus;
 };
 
 namespace {
 
-// Runs fn(i) for every member i on its own host thread (member 0 on the caller's), each thread bound for the call to
-// the NUMA node of its member's device (round 5: the staging it fills and the PCIe link it drives are there; the
-// caller's own affinity and memory policy come back when member 0 is done); first error wins.
+// Member i's host node and CPU list (cached; refreshed if the member's context was moved to another node).
+const std::vector<int>* member_cpus(kvsep_crc32c_group* g, int i, int* node) {
+  *node = kvsep::ctx_host_node(g->ctx[i]);
+  std::lock_guard<std::mutex> lk(g->node_mu);
+  if (g->node[i] != *node) {
+    g->node[i] = *node;
+    g->node_cpus[i] = kvsep::numa::node_cpus(*node);
+  }
+  return &g->node_cpus[i];
+}
+
+// Runs fn(i) for every member i on its own host thread (member 0 on the caller's); first error wins.  bind: the host
+// forms, which fill pinned staging and drive the member's PCIe link -- each thread is bound for the call to the NUMA
+// node of its member's device (round 5; the caller's own affinity and memory policy come back when member 0 is done).
+// The device-resident forms touch no host memory of their own and run unbound.
 template <typename Fn>
-int fan_out(kvsep_crc32c_group* g, Fn&& fn) {
+int fan_out(kvsep_crc32c_group* g, bool bind, Fn&& fn) {
   const int n = int(g->ctx.size());
   std::vector<int> rc(n, KVSEP_OK);
   std::vector<std::string> err(n);
   std::vector<std::thread> th;
   auto member = [&](int i) {
-    kvsep::numa::ScopedBind bind(kvsep::ctx_host_node(g->ctx[i]));
+    int node = -1;
+    const std::vector<int>* cpus = bind ? member_cpus(g, i, &node) : nullptr;
+    kvsep::numa::ScopedBind sb(bind ? node : -1, cpus);
     rc[i] = fn(i);
     if (rc[i]) err[i] = kvsep_last_error();  // the error text is thread-local
   };
@@ -116,6 +134,8 @@ int kvsep_crc32c_group_create(const int* devices, int ndev, kvsep_crc32c_group**
     g->ctx.push_back(c);
     g->stream.push_back(s);
     g->d_res.push_back(res);
+    g->node.push_back(-2);  // not read yet (member_cpus)
+    g->node_cpus.emplace_back();
   }
   *out = g;
   return KVSEP_OK;
@@ -152,7 +172,7 @@ int kvsep_crc32c_group_batch_host_span(kvsep_crc32c_group* g, const char* host_b
   std::vector<uint64_t> bounds(n + 1);
   int rc = kvsep_crc32c_partition(len, count, n, bounds.data());
   if (rc) return rc;
-  return fan_out(g, [&](int i) {
+  return fan_out(g, true, [&](int i) {
     const uint64_t b0 = bounds[i], b1 = bounds[i + 1];
     if (b0 == b1) return int(KVSEP_OK);
     return kvsep_crc32c_batch_host_span(g->ctx[i], host_base, span_bytes, off + b0, len + b0, init ? init + b0 : nullptr,
@@ -224,7 +244,7 @@ int kvsep_crc32c_group_verify_device(kvsep_crc32c_group* g, const void* const* b
   std::lock_guard<std::mutex> lk(g->mu);
   const int n = int(g->ctx.size());
   std::vector<uint64_t> fb(n, UINT64_MAX), nb(n, 0);
-  const int rc = fan_out(g, [&](int i) {
+  const int rc = fan_out(g, false, [&](int i) {
     if (!count[i]) return int(KVSEP_OK);
     kvsep::DeviceGuard dg(g->devices[i]);
     if (dg.err != hipSuccess) {

@@ -16,7 +16,8 @@ namespace kvsep {
 // Device scratch of one in-flight batch: the piece plan (planned mode), the work counter, the verify
 // defaults and the SST-verify arrays.  A scratch object is reused call after call; `last_use` orders a
 // call on a different stream behind the previous user, so reuse across streams is race-free.  The host
-// pipeline gives each staging slot its own Scratch so the two slots' batches overlap.
+// pipeline gives each staging slot its own Scratch so the two slots' batches overlap, and every graph capture takes a
+// capture set's Scratch of its own (crc32c_device.hip, capture_scratch).
 struct Scratch {
   uint64_t cap_count = 0, cap_pieces = 0;
   uint64_t* d_counts = nullptr;
@@ -26,9 +27,10 @@ struct Scratch {
   void* d_scan_tmp = nullptr;
   size_t scan_tmp_bytes = 0;
   uint32_t* d_counter = nullptr;
-  unsigned long long* d_verify = nullptr;  // [first_bad, nbad] when the caller passes none, then the accumulator sets
-  uint32_t vacc_next = 0;                   // captured verify calls take accumulator sets 1..7 in turn
-  uint32_t vacc_dirty = 0;                  // sets a failed call may have posted to: reset before their next use
+  unsigned long long* d_verify = nullptr;  // [first_bad, nbad] when the caller passes none, then the accumulator set
+  bool vacc_dirty = false;                  // a failed eager call may have posted to the set: reset before its next use
+  unsigned long long* d_vslot = nullptr;    // captured verify calls: one verdict slot (2 words) per publishing workgroup
+  uint32_t cap_vslot = 0;
   uint64_t* d_sst_len1 = nullptr;           // SST verify: len + 1 ...
   uint32_t* d_sst_stored = nullptr;         // ... and the stored trailer words
   uint64_t cap_sst = 0;

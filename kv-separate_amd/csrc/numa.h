@@ -106,9 +106,8 @@ inline std::vector<int> thread_cpus() {
 }
 
 // CPUs of `node` this thread may run on (sorted); empty if none / unknown.
-inline std::vector<int> node_cpus_allowed(int node, const std::vector<int>& allowed) {
+inline std::vector<int> cpus_allowed(const std::vector<int>& nc, const std::vector<int>& allowed) {
   std::vector<int> out;
-  const std::vector<int> nc = node_cpus(node);
   for (int c : nc)
     for (int a : allowed)
       if (a == c) {
@@ -116,6 +115,10 @@ inline std::vector<int> node_cpus_allowed(int node, const std::vector<int>& allo
         break;
       }
   return out;
+}
+
+inline std::vector<int> node_cpus_allowed(int node, const std::vector<int>& allowed) {
+  return cpus_allowed(node_cpus(node), allowed);
 }
 
 inline bool set_affinity(pid_t tid, const std::vector<int>& cpus) {
@@ -151,10 +154,11 @@ inline int page_node(const void* p) {
 // none of the thread's CPUs.
 class ScopedBind {
  public:
-  explicit ScopedBind(int node) {
+  // node_list: the node's CPUs as the caller cached them (null: read from sysfs now)
+  explicit ScopedBind(int node, const std::vector<int>* node_list = nullptr) {
     if (node < 0 || node >= kMaxNodes) return;
     prev_cpus_ = thread_cpus();
-    cpus_ = node_cpus_allowed(node, prev_cpus_);
+    cpus_ = node_list ? cpus_allowed(*node_list, prev_cpus_) : node_cpus_allowed(node, prev_cpus_);
     if (cpus_.empty() || !set_affinity(0, cpus_)) {
       cpus_.clear();
       return;

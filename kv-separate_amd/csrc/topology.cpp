@@ -45,7 +45,7 @@ int kvsep_device_numa_node(int device) {
 
 int kvsep_numa_node_cpus(int node, int* cpus, int cap) {
   const std::vector<int> c = kvsep::numa::node_cpus(node);
-  for (int i = 0; i < cap && i < int(c.size()); ++i) cpus[i] = c[i];
+  for (int i = 0; cpus && i < cap && i < int(c.size()); ++i) cpus[i] = c[i];  // (cpus may be null: count only)
   return int(c.size());
 }
 

@@ -71,6 +71,9 @@ _SIGS = {
     "kvsep_crc32c_ctx_set_schedule": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "kvsep_crc32c_ctx_set_kernel": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "kvsep_crc32c_reserve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]),
+    "kvsep_crc32c_reserve_captures": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "kvsep_crc32c_release_captures": (ctypes.c_int, [ctypes.c_void_p]),
+    "kvsep_crc32c_capture_sets": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "kvsep_crc32c_ctx_set_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "kvsep_crc32c_ctx_get_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                                    ctypes.POINTER(ctypes.c_uint64)]),
@@ -299,11 +302,27 @@ class Context:
         return {"device_node": dn.value, "staging_node": sn.value, "copier_cpus": list(cpus[:min(n, 4096)])}
 
     def inject_failure(self):
-        """Fault injection (tests): the next batched call fails right after enqueuing its CRC kernel."""
+        """Fault injection (tests; csrc/kvsep_testing.h): the next batched call fails right after enqueuing its CRC
+        kernel.  The library honours it only under KVSEP_TEST_HOOKS=1 (tests/conftest.py sets it)."""
         _check(lib().kvsep_crc32c_ctx_inject_failure(self._h), "inject_failure")
 
     def reserve(self, count: int, total_bytes: int):
         _check(lib().kvsep_crc32c_reserve(self._h, count, total_bytes), "reserve")
+
+    def reserve_captures(self, nsets: int):
+        """At least `nsets` capture sets (one per graph capture that may be held at once)."""
+        _check(lib().kvsep_crc32c_reserve_captures(self._h, nsets), "reserve_captures")
+
+    def release_captures(self):
+        """Every capture set free again: only once the graphs captured so far are destroyed."""
+        _check(lib().kvsep_crc32c_release_captures(self._h), "release_captures")
+
+    def capture_sets(self):
+        """(number of capture sets, how many a graph holds)."""
+        held = ctypes.c_int(0)
+        n = lib().kvsep_crc32c_capture_sets(self._h, ctypes.byref(held))
+        _check(n if n < 0 else 0, "capture_sets")
+        return n, held.value
 
     def kernel_name(self, count: int, max_len: int, total_bytes: int = 0) -> str:
         """The main kernel a batch of `count` blocks with these max_len / total_bytes hints runs on."""

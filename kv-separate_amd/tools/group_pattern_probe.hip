@@ -8,6 +8,9 @@
 //   1 1 KiB rows  the group read as 32 contiguous 1 KiB rows (the wide kernel's / the ceiling's row shape)
 //   2 2-line slots each instruction reads two consecutive 128-B lines of 4 of the group's blocks (16 lanes per block)
 //   3 stream      stream_read_kernel's pattern: the workgroup's 8 waves interleave 1 KiB rows of its 1 MiB run
+//   4-7 (round 6) slot rows with each block's rows read in a rotated order -- by 4 rows per slot, per wave, per
+//                 workgroup, or by 16 rows on every other wave -- so the lines in flight do not all sit at one offset
+//                 in their 4 KiB blocks (is config 2's deficit address-channel camping?)
 // kRows loads in flight per wave (issued together, then consumed), as the kernels' row groups.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o group_pattern_probe group_pattern_probe.hip
 // Usage: group_pattern_probe [MiB]
@@ -61,6 +64,11 @@ __global__ void __launch_bounds__(512) pattern_kernel(uintptr_t src, uint64_t nb
           const uint32_t row = r + u;
           uintptr_t a;
           if (kMode == 0) a = gb + (lane >> 3) * kBlock + row * 128u + (lane & 7u) * 16u;
+          else if (kMode >= 4) {  // round 6: slot rows with the row order rotated per slot / wave / workgroup
+            const uint32_t rot = kMode == 4 ? 4u * (lane >> 3) : kMode == 5 ? 4u * w : kMode == 6 ? 4u * (blockIdx.x & 7u)
+                                                                                            : 16u * (w & 1u);
+            a = gb + (lane >> 3) * kBlock + ((row + rot) & 31u) * 128u + (lane & 7u) * 16u;
+          }
           else if (kMode == 1) a = gb + row * 1024u + lane * 16u;
           else a = gb + ((row & 1u) * 4u + (lane >> 4)) * kBlock + (row >> 1) * 256u + (lane & 15u) * 16u;
           v[u] = ldnt(a);
@@ -114,12 +122,14 @@ int main(int argc, char** argv) {
   CK(hipStreamCreate(&st));
   const uintptr_t s = reinterpret_cast<uintptr_t>(d);
   for (int round = 0; round < 3; ++round) {
-    const double t[8] = {time_us<0, 4>(s, n, sink, st), time_us<0, 8>(s, n, sink, st), time_us<1, 4>(s, n, sink, st),
-                         time_us<1, 8>(s, n, sink, st), time_us<2, 4>(s, n, sink, st), time_us<2, 8>(s, n, sink, st),
-                         time_us<3, 4>(s, n, sink, st), time_us<3, 8>(s, n, sink, st)};
-    const char* nm[8] = {"slot rows x4", "slot rows x8", "1KiB rows x4", "1KiB rows x8", "2-line slots x4",
-                         "2-line slots x8", "stream x4", "stream x8"};
-    for (int i = 0; i < 8; ++i)
+    const double t[12] = {time_us<0, 4>(s, n, sink, st), time_us<0, 8>(s, n, sink, st), time_us<1, 4>(s, n, sink, st),
+                          time_us<1, 8>(s, n, sink, st), time_us<2, 4>(s, n, sink, st), time_us<2, 8>(s, n, sink, st),
+                          time_us<3, 4>(s, n, sink, st), time_us<3, 8>(s, n, sink, st), time_us<4, 4>(s, n, sink, st),
+                          time_us<5, 4>(s, n, sink, st), time_us<6, 4>(s, n, sink, st), time_us<7, 4>(s, n, sink, st)};
+    const char* nm[12] = {"slot rows x4", "slot rows x8", "1KiB rows x4", "1KiB rows x8", "2-line slots x4",
+                          "2-line slots x8", "stream x4", "stream x8", "slot rows x4 rot/slot", "slot rows x4 rot/wave",
+                          "slot rows x4 rot/wg", "slot rows x4 half/wave"};
+    for (int i = 0; i < 12; ++i)
       std::printf("{\"round\": %d, \"mib\": %llu, \"pattern\": \"%s\", \"us\": %.2f, \"TBps\": %.3f}\n", round,
                   (unsigned long long)mib, nm[i], t[i], double(n) / (t[i] * 1e-6) / 1e12);
     std::fflush(stdout);

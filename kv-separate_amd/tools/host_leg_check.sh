@@ -9,7 +9,6 @@ grep -m1 "^flags" /proc/cpuinfo | tr ' ' '\n' | grep -E "^(avx512f|vpclmulqdq|pc
 for m in default sse42; do
   KVSEP_HOST_CRC=$m timeout -k 10 120 ./kv-separate_amd/tools/host_leg_bench 1024 > gpurun_out/host_leg/host_leg_$m.jsonl || exit 1
 done
-timeout -k 10 120 ./kv-separate_amd/tools/fold_variants_probe > gpurun_out/host_leg/fold_variants.jsonl || exit 1
 timeout -k 10 300 python -u kv-separate_amd/tools/dbbench_crc32c.py > gpurun_out/host_leg/dbbench_crc32c.json || exit 1
 timeout -k 10 300 python -u kv-separate_amd/tools/dropin_probe.py gpurun_out/host_leg/dropin_crossover.json \
   > gpurun_out/host_leg/dropin_crossover.jsonl || exit 1

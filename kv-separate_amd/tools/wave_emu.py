@@ -997,12 +997,13 @@ class Workgroup:
 
 
 # ------------------------------------------------------------------------------------------------------------------
-# PiecesArgs (csrc/crc32c_device.hip) field offsets; the hidden arguments follow the 176-byte struct
+# PiecesArgs (csrc/crc32c_fold.inc) field offsets; the hidden arguments follow the 184-byte struct
 PIECES_ARGS = {"base": 0, "off": 8, "len": 16, "init": 24, "out": 32, "count": 40, "pstart": 48, "pblk": 56,
                "partial": 64, "work_counter": 72, "piece_bytes": 80, "zpiece": 88, "max_pieces": 96,
                "static_contig": (104, "<I"), "guided_div": (108, "<I"), "guided_cap": (112, "<I"), "hint": 120,
-               "expect": 128, "first_bad": 136, "nbad": 144, "tabs": 152, "vacc": 160}
-ARGS_BYTES = 168
+               "expect": 128, "first_bad": 136, "nbad": 144, "tabs": 152, "vacc": 160, "vslot": 168,
+               "vslot_base": (176, "<I")}
+ARGS_BYTES = 184
 # the verify accumulators (crc32c_device.hip, PiecesArgs::vacc): u64 words; [0] lowest block, [1] final arrival word
 # (arrived << 40) | mismatches, shard s's arrival word at [16 (s + 1)] (the combine kernel's two-level arrival)
 VACC_STRIDE, VACC_SHARDS = 16, 8
@@ -1106,21 +1107,39 @@ def batch_results(mem: Memory, f: dict, published: bool = True):
     return out, out != SENTINEL, (-1 if fb == (1 << 64) - 1 else fb), nb
 
 
+def alloc_slots(mem: Memory, f: dict, n: int):
+    """Verdict slots of a captured verify call (PiecesArgs::vslot, round 6): n (lowest block, count) pairs, sentinel-
+    filled so an unwritten slot shows."""
+    f["vslot"] = mem.alloc(16 * n, data=np.full(2 * n, SENTINEL, np.uint64))
+
+
+def slots(mem: Memory, f: dict, n: int):
+    v = mem.view(f["vslot"], 16 * n).view(np.uint64).reshape(n, 2)
+    return [(int(a), int(b)) for a, b in v]
+
+
 def run_batch_kernel(asm: str, name: str, threads: int, data: np.ndarray, off, ln, tabs: bytes, wg: int = 0,
                      grid: int = 256, hint: int = 0, expect=None, lds_bytes: int = 160768, last: bool = True,
-                     state: dict | None = None, init=None, shards: int = 1):
+                     state: dict | None = None, init=None, shards: int = 1, vslot: bool = False):
     """Run workgroup `wg` of a batch kernel (a PiecesArgs kernel in static, unplanned mode) over the given batch.
     Verify form: with `last` the other grid - 1 workgroups count as arrived, so this one publishes the verdict; without
-    it, it is an early one and `state` (a dict) receives the accumulators it leaves.
+    it, it is an early one and `state` (a dict) receives the accumulators it leaves.  vslot: a captured call's form --
+    the workgroup writes its verdict slot (state["slots"]: every slot of the grid) and touches neither the
+    accumulators nor the caller's words.
     Returns (out words, mask of blocks written, first_bad or -1, nbad, instructions executed)."""
-    mem, f = batch_memory(data, off, ln, tabs, expect, last_of=(wg, grid) if last else None, shards=shards)
+    mem, f = batch_memory(data, off, ln, tabs, expect, last_of=(wg, grid) if last and not vslot else None,
+                          shards=shards)
     f["hint"] = hint
+    if vslot:
+        alloc_slots(mem, f, grid)
     if init is not None:  # per-block initial CRCs (Extend(init[i], block i))
         f["init"] = mem.alloc(4 * len(init), data=np.asarray(init, np.uint32))
     steps = launch(mem, asm, name, threads, lds_bytes, f, grid, [wg])
     if state is not None and "vacc" in f:
         state["vacc"] = accumulators(mem, f)
-    return batch_results(mem, f, published=last) + (steps,)
+    if state is not None and vslot:
+        state["slots"] = slots(mem, f, grid)
+    return batch_results(mem, f, published=last or vslot) + (steps,)
 
 
 # DevTables field offsets (bytes), csrc/crc32c_device.hip
@@ -1128,11 +1147,13 @@ TAB_ZSMALL = 4096 * 9 + 1024 + 4096   # z1024, z4, ztree[6], byte1, zpiece, znar
 
 
 def run_planned_batch(asm: str, pieces: str, combine: str, data: np.ndarray, off, ln, tabs: bytes, piece_k: int = 0,
-                      grid: int = 256, expect=None):
+                      grid: int = 256, expect=None, state: dict | None = None):
     """One planned (split-block) call as launch_batch_in issues it: the piece table built on the host exactly as
     crc32c_plan_count_kernel / InclusiveSum / crc32c_plan_expand_kernel build it, the pieces kernel (dynamic
     schedule; one workgroup takes every item), then every workgroup of the combine kernel.  Pieces are
-    zsmall[piece_k]'s 16 KiB << piece_k.  Returns (out, written, first_bad, nbad, instructions)."""
+    zsmall[piece_k]'s 16 KiB << piece_k.  state (a dict, verify form): the call as captured -- verdict slots, the
+    combine kernel's after the pieces kernel's (vslot_base = grid); state["slots"] receives them all.
+    Returns (out, written, first_bad, nbad, instructions)."""
     ln = np.asarray(ln, np.uint64)
     n = ln.size
     P = (16 * 1024) << piece_k
@@ -1147,8 +1168,15 @@ def run_planned_batch(asm: str, pieces: str, combine: str, data: np.ndarray, off
              zpiece=f["tabs"] + TAB_ZSMALL + 4096 * piece_k, guided_div=0, guided_cap=0)
     # one workgroup takes every item; not workgroup 0, so its shard (5) is one the combine grid below may not have:
     # the planned kernel's counts must reach the publishing grid anyway
+    cgrid = min((n + 255) // 256, 2048)  # kCombineMaxGrid
+    if state is not None:
+        alloc_slots(mem, f, grid + cgrid)
     steps = launch(mem, asm, pieces, 512, 160768, f, grid, [5])
-    steps += launch(mem, asm, combine, 256, 4096, f, (n + 255) // 256)
+    if state is not None:
+        f["vslot_base"] = grid
+    steps += launch(mem, asm, combine, 256, 4096, f, cgrid)
+    if state is not None:
+        state["slots"] = slots(mem, f, grid + cgrid)
     return batch_results(mem, f) + (steps,)
 
 

@@ -8,6 +8,8 @@ import sys
 import pytest
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+# arms the library's test-only hooks (csrc/kvsep_testing.h: fault injection); the shipped library ignores them otherwise
+os.environ.setdefault("KVSEP_TEST_HOOKS", "1")
 sys.path.insert(0, os.path.join(ROOT, "kv-separate_amd"))
 sys.path.insert(0, ROOT)
 

@@ -76,6 +76,15 @@ int main() {
   }
   CHECK(numa::thread_cpus() == before);  // the scope restores the caller's affinity
   {
+    // a cached CPU list (the group's members): bound to that list, intersected with the thread's CPUs,
+    // without reading sysfs
+    const std::vector<int> cached{5, 6, 42};
+    numa::ScopedBind c(1, &cached);
+    CHECK(c.bound());
+    CHECK((numa::thread_cpus() == std::vector<int>{5, 6}));
+  }
+  CHECK(numa::thread_cpus() == before);
+  {
     numa::ScopedBind none(9);  // unknown node: nothing changes
     CHECK(!none.bound());
     CHECK(numa::thread_cpus() == before);

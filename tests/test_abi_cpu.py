@@ -46,18 +46,27 @@ def test_engine_library_does_not_export_the_leveldb_symbol():
 
 
 def test_abi_version():
-    assert kvsep.lib().kvsep_abi_version() == 3
-    assert "ABI 3" in kvsep.build_info()
+    assert kvsep.lib().kvsep_abi_version() == 4
+    assert "ABI 4" in kvsep.build_info()
 
 
 def test_no_environment_variable_reaches_the_kernel_choice():
     """The shipped library reads no variant / kernel-routing variable (those exist only in the KVSEP_DIAG tools
     build): only KVSEP_STRICT_GPU, KVSEP_COPY_THREADS, KVSEP_HOST_CRC (=sse42 / =portable: a slower host leg, for
-    A/B) and KVSEP_SYSFS_ROOT (where the topology is read: tests fake it), none of which can change a CRC."""
+    A/B), KVSEP_SYSFS_ROOT (where the topology is read: tests fake it) and KVSEP_TEST_HOOKS (=1 arms the test-only
+    fault injection of csrc/kvsep_testing.h), none of which can change a CRC."""
     import re
     strings = open(kvsep.LIB_PATH, "rb").read()
     names = set(re.findall(rb"KVSEP_[A-Z_]{3,}", strings))
-    assert names <= {b"KVSEP_STRICT_GPU", b"KVSEP_COPY_THREADS", b"KVSEP_HOST_CRC", b"KVSEP_SYSFS_ROOT"}, names
+    assert names <= {b"KVSEP_STRICT_GPU", b"KVSEP_COPY_THREADS", b"KVSEP_HOST_CRC", b"KVSEP_SYSFS_ROOT",
+                     b"KVSEP_TEST_HOOKS"}, names
+
+
+def test_fault_injection_is_not_public_and_needs_the_test_environment():
+    """the fault-injection hook is not in the public header, and the library refuses it without
+    KVSEP_TEST_HOOKS=1 (checked before any device is touched: a null context is refused either way)."""
+    assert "kvsep_crc32c_ctx_inject_failure" not in kvsep.header_functions()
+    assert kvsep.lib().kvsep_crc32c_ctx_inject_failure(None) == -1
 
 
 def test_python_extend_rejects_n_past_buffer():

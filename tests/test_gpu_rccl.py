@@ -115,3 +115,19 @@ def test_bench_verify_form_one_rank_rccl():
     v = line["verify"]
     assert line["form"] == "verify" and v["ok"] and v["nbad"] == 2 and v["first_bad"] == 13, v
     assert line["parity"]["mismatches"] == 0 and line["parity"]["every_block_checked"], line["parity"]
+
+
+def test_bench_wrong_result_exits_nonzero():
+    """one gathered result word corrupted (test hook KVSEP_BENCH_CORRUPT_RESULT=<rank>) makes the
+    reference check fail -- bench.py still prints the line, with the reason in `failures`, and exits non-zero, so a
+    driver reading rc never records it as a clean number."""
+    env = _env()
+    env["KVSEP_BENCH_CORRUPT_RESULT"] = "0"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", "2", "--steps", "2", "--warmup", "1", "--no-cpu",
+           "--pmc-live", "off", "--roundtrip-gib", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 1, (r.returncode, r.stderr[-3000:])
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["parity"]["all_blocks_match"] is False and line["parity"]["mismatches"] == 1, line["parity"]
+    assert len(line["failures"]) == 1 and line["failures"][0].startswith("parity"), line["failures"]
+    assert line["value"] > 0  # the measurement itself is still reported

@@ -5,7 +5,8 @@ instruction by instruction -- 64-lane VGPRs under EXEC, SGPRs, LDS, scalar / vec
 for one workgroup of the real 256-workgroup grid, and the CRCs it writes are compared with the oracle.  Round 3's
 sorted-window fault was a code-generation error of exactly this kind (a rematerialised table base restored under the
 narrowed EXEC of a nested divergent branch, so the slot-end lanes of every later group read the wrong table); the
-emulator reproduces it from the diag build's assembly (tools/sorted_vin_emulate.py) and this test runs the same check
+emulator reproduced it from the diag build's assembly (tools/sorted_vin_emulate.py, retired in round 6: commit 8853f41) and
+this test runs the same check
 on every shipped narrow-family kernel, plain and verify forms, so a miscompile of that class fails on the CPU.  The
 wide kernel runs too: unplanned (static runs, one workgroup of the grid) and planned (host-built piece table exactly
 as the plan kernels build it, the guided schedule, then every workgroup of the combine kernel).
@@ -31,8 +32,8 @@ sys.path.insert(0, PKG)
 SORTED = "_ZN5kvsep27crc32c_narrow_sorted_kernelILi4ELb1ELi1024ELb%dENS_5ExactEEEvNS_10PiecesArgsE"
 NARROW16 = "_ZN5kvsep20crc32c_narrow_kernelILi4ELb1ELi1024ELb0ELb1ENS_7LdsFullELb%dENS_5ExactEEEvNS_10PiecesArgsE"
 NARROW8 = "_ZN5kvsep20crc32c_narrow_kernelILi4ELb1ELi512ELb1ELb1ENS_7LdsFullELb%dENS_5ExactEEEvNS_10PiecesArgsE"
-CLAIM = "_ZN5kvsep26crc32c_narrow_claim_kernelILi4ELi512ELb%dELb1ELi8EEEvNS_10PiecesArgsE"
-CLAIM16 = "_ZN5kvsep26crc32c_narrow_claim_kernelILi4ELi512ELb%dELb1ELi16EEEvNS_10PiecesArgsE"
+CLAIM = "_ZN5kvsep26crc32c_narrow_claim_kernelILi4ELi512ELb%dELb1ELi8ELj3EEEvNS_10PiecesArgsE"  # kLean 3 (round 6)
+CLAIM16 = "_ZN5kvsep26crc32c_narrow_claim_kernelILi4ELi512ELb%dELb1ELi16ELj0EEEvNS_10PiecesArgsE"
 # (label, template, threads per workgroup, arrival levels of the verify publish: 8 = per-XCD shards, then the final word)
 KERNELS = [("sorted", SORTED, 1024, 1), ("narrow16", NARROW16, 1024, 1), ("narrow8", NARROW8, 512, 1),
            ("claim", CLAIM, 512, 8), ("claim16", CLAIM16, 512, 8)]
@@ -92,6 +93,15 @@ def test_emulated_kernel_matches_oracle(env, label, tmpl, threads, shards, kind)
                                            shards=shards)
         assert (fb, nb) == (int(mine.min()), int(mine.size))
     _verify_tail(E, tmpl % 1, threads, data, off, ln, tabs, wg, hint, exp, mask, mine, plant, shards=shards)
+    # the captured form (round 6): the workgroup's verdict in its own slot, nothing published, no accumulator touched
+    st = {}
+    out_s, written_s, fb, nb, _ = E.run_batch_kernel(ASM, tmpl % 1, threads, data, off, ln, tabs, wg=wg, hint=hint,
+                                                     expect=stored, shards=shards, vslot=True, state=st)
+    assert np.array_equal(np.nonzero(written_s)[0], mine) and np.array_equal(out_s[mine], exp[mine])
+    assert (fb, nb) == (E.SENTINEL, E.SENTINEL)
+    sl = st["slots"]
+    assert sl[wg] == (int(plant.min()), 3), sl[wg]
+    assert all(v == (E.SENTINEL, E.SENTINEL) for i, v in enumerate(sl) if i != wg)
 
 
 def _verify_tail(E, name, threads, data, off, ln, tabs, wg, hint, exp, mask, mine, plant, lds_bytes=160768, shards=1):
@@ -180,6 +190,19 @@ def test_emulated_wide_planned_with_combine(env, verify):
     assert np.array_equal(out, exp), f"{np.count_nonzero(out != exp)} wrong CRCs"
     if verify:
         assert (fb, nb) == (2, 3)  # the combine kernel's last workgroup published; accumulators reset (batch_results)
+        # captured: the pieces kernel's workgroup 5 (the whole blocks) and the combine kernel's one workgroup (the
+        # split ones) each write their slot, clean or not; the reduce kernel's min / sum over the slots is the verdict
+        st = {}
+        out_s, _, fb, nb, _ = E.run_planned_batch(ASM, PIECES % (1, 1, 1), COMBINE % 1, data, off, ln, tabs,
+                                                  expect=expect, state=st)
+        assert np.array_equal(out_s, exp) and (fb, nb) == (E.SENTINEL, E.SENTINEL)
+        sl = st["slots"]
+        split = set(np.nonzero(ln >= 2 * 16 * 1024)[0].tolist())
+        whole = [int(b) for b in plant if int(b) not in split]
+        assert sl[5] == ((min(whole), len(whole)) if whole else ((1 << 64) - 1, 0)), sl[5]
+        assert sl[256] == (min(int(b) for b in plant if int(b) in split), len(plant) - len(whole)), sl[256]
+        written = [v for v in sl if v != (E.SENTINEL, E.SENTINEL)]
+        assert len(written) == 2 and min(v[0] for v in written) == 2 and sum(v[1] for v in written) == 3
         _, _, fb, nb, _ = E.run_planned_batch(ASM, PIECES % (1, 1, 1), COMBINE % 1, data, off, ln, tabs,
                                               expect=_planted(exp, mask, np.array([], np.int64)))
         assert (fb, nb) == (-1, 0)
