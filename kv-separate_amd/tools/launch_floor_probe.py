@@ -40,6 +40,9 @@ def graph_avg_us(fn, reps=20, rounds=3):
         e1.record()
         torch.cuda.synchronize()
         best.append(e0.elapsed_time(e1) * 1e3 / reps)
+    del g  # the graph is gone: every context's capture sets may serve the next capture
+    for c in ctxs.values():
+        c.release_captures()
     return min(best), sorted(best)[len(best) // 2]
 
 

@@ -75,7 +75,7 @@ def parity(ctxs):
     return ok
 
 
-def graph_us(fn, reps=20):
+def graph_us(fn, ctx, reps=20):
     fn()
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
@@ -89,6 +89,8 @@ def graph_us(fn, reps=20):
     g.replay()
     e1.record()
     torch.cuda.synchronize()
+    del g  # the graph is gone: its capture set may serve the next capture
+    ctx.release_captures()
     return e0.elapsed_time(e1) * 1e3 / reps
 
 
@@ -120,7 +122,7 @@ def main():
             for v in variants:
                 times[v].append(graph_us(lambda v=v: ctxs[v].batch_device(
                     data.data_ptr(), d_off, d_len, outs[v], count=count, total_bytes=total, max_len=args.block,
-                    stream=torch.cuda.current_stream())))
+                    stream=torch.cuda.current_stream()), ctxs[v]))
         ref = outs[variants[0]].cpu()
         for v in variants:
             t = sorted(times[v])

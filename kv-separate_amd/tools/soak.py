@@ -159,6 +159,8 @@ def soak(seed, seconds=None, max_cases=None, log=print, pool=POOL):
                 g.replay()
                 torch.cuda.synchronize()
                 got = out.cpu().numpy().view(np.uint32)
+                del g  # the graph is gone: its capture set may serve the next capture (kvsep_crc32c_release_captures)
+                ctx.release_captures()
             mism = int(np.count_nonzero(np.asarray(got, np.uint32) != exp))
             cases += 1
             blocks += n

@@ -76,6 +76,8 @@ def graph_us(fn, reps=20, rounds=7):
         e1.record()
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1) * 1e3 / reps)
+    del g  # the graph is gone: its capture set may serve the next capture
+    ctx.release_captures()
     return sorted(ts)[len(ts) // 2]
 
 
