@@ -92,7 +92,9 @@ int kvsep_crc32c_ctx_set_schedule(kvsep_crc32c_ctx* ctx, int dynamic);
  * kernel whenever max_len <= 64 KiB, 3 / 4 = as 2 with 16- / 8-wave workgroups, 5 = as 2 in the sorted-window form,
  * 6 = as 2 with each workgroup's contiguous run of groups dealt to its waves by an LDS claim counter (round 4; auto
  * takes it for uniform batches of 32 Ki - 384 Ki blocks <= 4 KiB, 32 Ki - 64 Ki blocks of 4-8 KiB), 7 = as 6 with
- * 16 lanes per block, 4-block groups (auto: uniform batches of >= 4 Ki blocks of 8-12 KiB, up to 512 MiB).
+ * 16 lanes per block, 4-block groups (auto: uniform batches of >= 4 Ki blocks of 8-12 KiB, up to 512 MiB), 8 = the
+ * narrow kernel whose workgroup's 8 waves share each 8-block group (round 6; blocks over 4 KiB take its wide path;
+ * auto never picks it: 1.5x the claim kernel's time on 4 KiB blocks).
  * A choice of speed only: every kernel is exact for every block.  No environment variable changes it. */
 int kvsep_crc32c_ctx_set_kernel(kvsep_crc32c_ctx* ctx, int kernel);
 /* NUMA node the context's host legs are placed on: its pinned staging is allocated, and its copier threads run, on

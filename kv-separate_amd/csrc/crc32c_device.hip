@@ -279,13 +279,15 @@ bool claim16_route(uint64_t count, uint64_t total_bytes, uint64_t max_len) {
 // Narrow-kernel form of a batch that use_narrow() put on the narrow kernels: 6 = 16-wave workgroups, 9 = 8-wave
 // workgroups (fill overlapped with the first loads), 10 = workgroup-contiguous runs dealt by LDS claims
 // (crc32c_narrow_claim_kernel, 8 waves), 11 = the same with 16-lane slots, 20 = sorted windows
-// (crc32c_narrow_sorted_kernel, 16 waves).
+// (crc32c_narrow_sorted_kernel, 16 waves), 12 = the workgroup's 8 waves on one group (crc32c_narrow_coop_kernel;
+// set_kernel only: measured 1.5x the claim kernel's time on config 2, see its header).
 int narrow_form(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes, uint64_t max_len) {
   if (c->kernel == 3) return 6;
   if (c->kernel == 4) return 9;
   if (c->kernel == 5) return 20;
   if (c->kernel == 6) return 10;
   if (c->kernel == 7) return 11;
+  if (c->kernel == 8) return 12;
   // 16-wave workgroups below 128 Ki blocks of <= 8 KiB (32 Ki blocks of 8-32 KiB), 8-wave ones from there on.  A
   // small batch gives each wave only a couple of 8-block groups, and more waves hide more of the launch/first-load
   // ramp (256 MiB of 4 KiB blocks: 16 waves +2-5 %); a large one streams better with 8 (1 GiB of 4 KiB blocks:
@@ -561,16 +563,21 @@ int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, bool capt
     int nv = narrow_form(c, count, total_bytes, max_len);
     nv = diag_narrow_form(c, nv);  // KVSEP_DIAG build only
     a.hint = max_len;
-    if (expect && (nv == 6 || nv == 9 || nv == 10 || nv == 11 || nv == 20)) {  // verify form of the shipped forms
+    if (nv == 12 && a.hint > kCoopMaxLen) a.hint = kCoopMaxLen;  // its rows cover 4 KiB; longer blocks take its wide path
+    if (expect && (nv == 6 || nv == 9 || nv == 10 || nv == 11 || nv == 12 || nv == 20)) {  // the shipped forms' verify
       switch (nv) {
         case 9: crc32c_narrow_kernel<4, true, 512, true, true, LdsFull, true><<<grid, 512, 0, s>>>(a); break;
         case 10: crc32c_narrow_claim_kernel<4, 512, true, true, 8, kClaimLean><<<grid, 512, 0, s>>>(a); break;
         case 11: crc32c_narrow_claim_kernel<4, 512, true, true, 16><<<grid, 512, 0, s>>>(a); break;
+        case 12:
+          if (init) crc32c_narrow_coop_kernel<true, true><<<grid, 512, 0, s>>>(a);
+          else crc32c_narrow_coop_kernel<true, false><<<grid, 512, 0, s>>>(a);
+          break;
         case 20: crc32c_narrow_sorted_kernel<4, true, 1024, true><<<grid, 1024, 0, s>>>(a); break;
         default: crc32c_narrow_kernel<4, true, 1024, false, true, LdsFull, true><<<grid, 1024, 0, s>>>(a); break;
       }
     } else {
-    // KVSEP_DIAG variants only (the shipped forms are 6, 9, 10, 11 and 20): they post to the caller's words directly, from
+    // KVSEP_DIAG variants only (the shipped forms are 6, 9, 10, 11, 12 and 20): they post to the caller's words directly, from
     // their own in-kernel compare or from verify_finish_kernel, so those words are set first
     if (expect) {
       KVSEP_HIP(hipMemsetAsync(first_bad, 0xff, 8, s));
@@ -583,6 +590,10 @@ int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, bool capt
       case 9: crc32c_narrow_kernel<4, true, 512, true><<<grid, 512, 0, s>>>(a); break;
       case 10: crc32c_narrow_claim_kernel<4, 512, false, true, 8, kClaimLean><<<grid, 512, 0, s>>>(a); break;
       case 11: crc32c_narrow_claim_kernel<4, 512, false, true, 16><<<grid, 512, 0, s>>>(a); break;
+      case 12:
+        if (init) crc32c_narrow_coop_kernel<false, true><<<grid, 512, 0, s>>>(a);
+        else crc32c_narrow_coop_kernel<false, false><<<grid, 512, 0, s>>>(a);
+        break;
       case 20: crc32c_narrow_sorted_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
       default: crc32c_narrow_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
     }
@@ -723,7 +734,7 @@ int kvsep_crc32c_ctx_set_schedule(kvsep_crc32c_ctx* c, int dynamic) {
 }
 
 int kvsep_crc32c_ctx_set_kernel(kvsep_crc32c_ctx* c, int kernel) {
-  if (!c || kernel < 0 || kernel > 7) return set_err(KVSEP_EINVAL, "kernel must be 0..7");
+  if (!c || kernel < 0 || kernel > 8) return set_err(KVSEP_EINVAL, "kernel must be 0..8");
   std::lock_guard<std::mutex> g(c->mu);
   c->kernel = kernel;
   return KVSEP_OK;
@@ -934,7 +945,9 @@ const char* kvsep_crc32c_kernel_name(kvsep_crc32c_ctx* c, uint64_t count, uint64
   if (planned || !use_narrow(c, count, total_bytes, max_len)) return "crc32c_pieces_kernel";
   const int nf = narrow_form(c, count, total_bytes, max_len);
   return nf == 20 ? "crc32c_narrow_sorted_kernel"
-         : nf == 10 || nf == 11 ? "crc32c_narrow_claim_kernel" : "crc32c_narrow_kernel";
+         : nf == 10 || nf == 11 ? "crc32c_narrow_claim_kernel"
+         : nf == 12             ? "crc32c_narrow_coop_kernel"
+                                : "crc32c_narrow_kernel";
 }
 
 int kvsep_stream_read_device(kvsep_crc32c_ctx* c, void* stream, const void* src, uint64_t nbytes, uint32_t* sink) {

@@ -24,7 +24,7 @@ from conftest import load_oracle  # noqa: E402  (the checker)
 from kvsep import splitmix64_bytes  # noqa: E402
 
 POOL = 192 << 20
-KERNELS = ("auto", "wide", "narrow16", "narrow8", "sorted", "claim", "claim16")
+KERNELS = ("auto", "wide", "narrow16", "narrow8", "sorted", "claim", "claim16", "coop")
 
 
 def lengths(rng, n, kind):

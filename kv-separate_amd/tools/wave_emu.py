@@ -558,6 +558,16 @@ class Workgroup:
             w.sset(o[0], r)
             w.scc = int(r != 0)
             return
+        if op == 's_bfe_i32':
+            x, c = g(o[1]), g(o[2])
+            wd = (c >> 16) & 0x7F
+            r = (x >> (c & 31)) & ((1 << wd) - 1) if wd else 0
+            if wd and r >> (wd - 1) & 1:
+                r -= 1 << wd
+            r &= M32
+            w.sset(o[0], r)
+            w.scc = int(r != 0)
+            return
         if op == 's_bitset1_b32':
             w.sset(o[0], g(o[0]) | (1 << (g(o[1]) & 31)))
             return
@@ -858,7 +868,7 @@ class Workgroup:
             r = V(o[1]).astype(np.uint64) + V(o[2]).astype(np.uint64) + V(o[3]).astype(np.uint64)
             w.vset(o[0], (r & np.uint64(M32)).astype(np.uint32))
             return
-        if base in ('v_add_co_u32', 'v_sub_co_u32', 'v_addc_co_u32', 'v_subb_co_u32'):
+        if base in ('v_add_co_u32', 'v_sub_co_u32', 'v_subrev_co_u32', 'v_addc_co_u32', 'v_subb_co_u32'):
             dst, cd, a_t, b_t = o[0], o[1], o[2], o[3]
             a, b = V(a_t).astype(np.int64), V(b_t).astype(np.int64)
             cin = Wave.bits(w.sget(o[4], 64)).astype(np.int64) if len(o) > 4 else 0
@@ -870,6 +880,9 @@ class Workgroup:
                 co = r > M32
             elif base == 'v_sub_co_u32':
                 r = a - b
+                co = r < 0
+            elif base == 'v_subrev_co_u32':
+                r = b - a
                 co = r < 0
             else:
                 r = a - b - cin

@@ -54,14 +54,14 @@ def test_capture_and_replay(layout, oracle):
         ctx.close()
 
 
-@pytest.mark.parametrize("layout", ["planned", "unplanned", "narrow", "sorted", "claim", "claim16"])
+@pytest.mark.parametrize("layout", ["planned", "unplanned", "narrow", "sorted", "claim", "claim16", "coop"])
 def test_capture_verify_form(layout, oracle):
     """The verify form captured once and replayed: its verdict words are published by the last workgroup of the
     publishing kernel (the CRC kernel; the combine kernel for a split batch), which also resets the context's
     accumulators, so a verdict never leaks into the next replay: clean -> one bad record -> three bad records spread
     over the batch (several workgroups post) -> clean again, each replayed twice, two calls per replay."""
     kernel = {"planned": "auto", "unplanned": "wide", "narrow": "narrow16", "sorted": "sorted", "claim": "claim",
-              "claim16": "claim16"}[layout]
+              "claim16": "claim16", "coop": "coop"}[layout]
     if layout == "planned":
         off, ln = W.cfg3_layout(vlog=True, count=40)  # split blocks: the combine kernel publishes
         hint = 0

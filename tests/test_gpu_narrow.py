@@ -159,7 +159,7 @@ def test_sorted_windows_ragged(oracle, pool, count):
         ctx.close()
 
 
-@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted", "claim", "claim16"])
+@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted", "claim", "claim16", "coop"])
 @pytest.mark.parametrize("count", [70000, 200000])
 def test_verify_several_groups_per_wave(oracle, pool, kernel, count):
     """Verify form with several 8-block groups per wave (3 and 7 per 64-block window at these counts): the sorted
@@ -190,7 +190,7 @@ def test_verify_several_groups_per_wave(oracle, pool, kernel, count):
         ctx.close()
 
 
-@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted", "claim", "claim16"])
+@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted", "claim", "claim16", "coop"])
 def test_every_end_geometry(oracle, pool, kernel):
     """Every case of the slot's end path: m = 0..7 whole 16-B chunks between the 128-B grid and the 16-B end (m = 7
     uses all of lanes 0..6 of the tail load), each with head and tail bytes 0..15, with and without body rows.  The
@@ -218,7 +218,7 @@ def test_every_end_geometry(oracle, pool, kernel):
     assert np.array_equal(got, oracle.batch(data, off, ln, init))
 
 
-@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted", "claim", "claim16"])
+@pytest.mark.parametrize("kernel", ["narrow16", "narrow8", "sorted", "claim", "claim16", "coop"])
 def test_verify_mismatch_on_deferred_block(oracle, pool, kernel):
     """Verify form under an understated max_len: blocks longer than the hint leave their 8-block group and
     are checksummed by the deferred walk, whose compare is verify_uniform over the wave-uniform stored word.  Mismatches

@@ -242,7 +242,7 @@ def test_verify_mode_first_bad(ctx, oracle):
 
 
 @pytest.mark.parametrize("kernel,shape", [("wide", "4k"), ("narrow16", "4k"), ("narrow8", "4k"), ("claim", "4k"),
-                                          ("claim16", "8k"), ("sorted", "ragged"), ("auto", "split")])
+                                          ("claim16", "8k"), ("sorted", "ragged"), ("auto", "split"), ("coop", "4k")])
 def test_verify_every_block_bad(kernel, shape, oracle):
     """A batch whose every stored word is wrong (a corrupt table or vlog, table/format.cc:99-106): the verdict is block
     0 and the whole count, on every kernel form and through the combine kernel of a split batch.  Round 5 posts one
@@ -268,7 +268,7 @@ def test_verify_every_block_bad(kernel, shape, oracle):
         nb = torch.zeros(1, dtype=torch.int64, device=DEV)
         args = dict(total_bytes=int(ln.sum()), max_len=int(ln.max()))
         want_kernel = {"wide": "pieces", "narrow16": "narrow_kernel", "narrow8": "narrow_kernel", "claim": "claim",
-                       "claim16": "claim", "sorted": "sorted", "auto": "pieces"}[kernel]
+                       "claim16": "claim", "sorted": "sorted", "auto": "pieces", "coop": "coop"}[kernel]
         assert want_kernel in c.kernel_name(ln.size, args["max_len"], args["total_bytes"])
         c.batch_device(d.data_ptr(), dev_u64(off), dev_u64(ln), out, **args)
         torch.cuda.synchronize()

@@ -65,7 +65,7 @@ def test_wide_schedules_ragged(ragged, sched):
         ctx.close()
 
 
-@pytest.mark.parametrize("kernel", ["narrow", "narrow16", "narrow8", "sorted", "claim", "claim16"])
+@pytest.mark.parametrize("kernel", ["narrow", "narrow16", "narrow8", "sorted", "claim", "claim16", "coop"])
 def test_narrow_workgroups_ragged(ragged, kernel):
     d, off, ln, init, exp = ragged
     ctx = kvsep.Context(0)
@@ -78,7 +78,7 @@ def test_narrow_workgroups_ragged(ragged, kernel):
         ctx.close()
 
 
-@pytest.mark.parametrize("kernel", ["auto", "wide", "narrow16", "narrow8", "sorted", "claim", "claim16"])
+@pytest.mark.parametrize("kernel", ["auto", "wide", "narrow16", "narrow8", "sorted", "claim", "claim16", "coop"])
 def test_understated_hint_is_exact(ragged, kernel):
     """max_len = 4 KiB although blocks run to 40 KB: blocks over the hint are deferred (narrow) or whole (wide)."""
     d, off, ln, init, exp = ragged

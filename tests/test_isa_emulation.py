@@ -34,9 +34,12 @@ NARROW16 = "_ZN5kvsep20crc32c_narrow_kernelILi4ELb1ELi1024ELb0ELb1ENS_7LdsFullEL
 NARROW8 = "_ZN5kvsep20crc32c_narrow_kernelILi4ELb1ELi512ELb1ELb1ENS_7LdsFullELb%dENS_5ExactEEEvNS_10PiecesArgsE"
 CLAIM = "_ZN5kvsep26crc32c_narrow_claim_kernelILi4ELi512ELb%dELb1ELi8ELj3EEEvNS_10PiecesArgsE"  # kLean 3 (round 6)
 CLAIM16 = "_ZN5kvsep26crc32c_narrow_claim_kernelILi4ELi512ELb%dELb1ELi16ELj0EEEvNS_10PiecesArgsE"
+# the cooperative kernel (round 6, narrow form 12): the workgroup's 8 waves on one group, one barrier per group;
+# init-less template (kInit false: no init word loaded)
+COOP = "_ZN5kvsep25crc32c_narrow_coop_kernelILb%dELb0EEEvNS_10PiecesArgsE"
 # (label, template, threads per workgroup, arrival levels of the verify publish: 8 = per-XCD shards, then the final word)
 KERNELS = [("sorted", SORTED, 1024, 1), ("narrow16", NARROW16, 1024, 1), ("narrow8", NARROW8, 512, 1),
-           ("claim", CLAIM, 512, 8), ("claim16", CLAIM16, 512, 8)]
+           ("claim", CLAIM, 512, 8), ("claim16", CLAIM16, 512, 8), ("coop", COOP, 512, 8)]
 
 
 @pytest.fixture(scope="module")
