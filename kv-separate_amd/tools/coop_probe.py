@@ -3,7 +3,8 @@
 bit-exactness against the oracle first (ragged blocks at every offset mod 128 with per-block initial CRCs, blocks over
 the hint, empty blocks, a verify call with planted mismatches; every kernel must pass before its time means
 anything), then graph-replay launch times on uniform blocks, interleaved in one process over the same buffers.
-usage: coop_probe.py [--kernels claim,coop] [--sizes 128,256,1024] [--block 4096] [--rounds 5]"""
+usage: coop_probe.py [--kernels claim,coop] [--sizes 128,256,1024] [--block 4096] [--rounds 5] [--lib PATH]
+(--lib: another build of the library, e.g. an A/B copy of the same sources at another commit)"""
 import argparse
 import os
 import sys
@@ -111,7 +112,11 @@ def main():
     ap.add_argument("--block", type=int, default=4096)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--lib", default=None)
     args = ap.parse_args()
+    if args.lib:
+        kvsep.LIB_PATH = os.path.abspath(args.lib)
+    print(f"library {kvsep.LIB_PATH}", flush=True)
     kernels = args.kernels.split(",")
     ctxs = contexts(kernels)
     if not args.no_parity and not parity(ctxs):

@@ -13,6 +13,9 @@
 //                 in their 4 KiB blocks (is config 2's deficit address-channel camping?)
 //   8 (round 6)   slot rows with the workgroup's 8 waves on the same 8 blocks: wave w reads rows 4w..4w+3 of each, so
 //                 the workgroup's loads in flight sit in one 32 KiB window, as the streaming pattern's do
+//   9 (round 6)   as 8 with wave w on rows w, w + 8, w + 16, w + 24
+//   10, 11        slot rows with the waves in teams of 4 / 2, each team on its own group and each wave on a consecutive
+//                 share of the group's rows: 2 / 4 groups in flight per workgroup (64 / 128 KiB windows)
 // kRows loads in flight per wave (issued together, then consumed), as the kernels' row groups.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o group_pattern_probe group_pattern_probe.hip
 // Usage: group_pattern_probe [MiB]
@@ -44,7 +47,22 @@ __global__ void __launch_bounds__(512) pattern_kernel(uintptr_t src, uint64_t nb
   const uint64_t per = (groups + gridDim.x - 1) / gridDim.x;
   const uint64_t g0 = uint64_t(blockIdx.x) * per, g1 = g0 + per < groups ? g0 + per : groups;
   u32x4 acc = {0, 0, 0, 0};
-  if (kMode == 8 || kMode == 9) {  // round 6: slot rows, the workgroup's 8 waves on the SAME 8 blocks per round (32
+  if (kMode == 10 || kMode == 11) {  // round 6: the workgroup's waves in teams of 4 (10) or 2 (11), each team on its own
+    // group, wave t of a team reading its consecutive share of each block's 32 rows (8 or 16 rows, kRows at a time)
+    constexpr uint32_t kTeam = kMode == 10 ? 4 : 2, kTeams = 8 / kTeam, kShare = 32 / kTeam;
+    const uint32_t team = w / kTeam, t = w % kTeam;
+    for (uint64_t g = g0 + team; g < g1; g += kTeams) {
+      const uintptr_t gb = src + g * kGroup;
+      for (uint32_t r = 0; r < kShare; r += kRows) {
+        u32x4 v[kRows];
+#pragma unroll
+        for (int u = 0; u < kRows; ++u)
+          v[u] = ldnt(gb + (lane >> 3) * kBlock + (t * kShare + r + u) * 128u + (lane & 7u) * 16u);
+#pragma unroll
+        for (int u = 0; u < kRows; ++u) acc ^= v[u];
+      }
+    }
+  } else if (kMode == 8 || kMode == 9) {  // round 6: slot rows, the workgroup's 8 waves on the SAME 8 blocks per round (32
     // KiB window): wave w reads rows 4w .. 4w+3 (8) or rows w, w+8, w+16, w+24 (9) of each of the round's 8 blocks
     for (uint64_t g = g0; g < g1; ++g) {
       const uintptr_t gb = src + g * kGroup;
@@ -137,15 +155,17 @@ int main(int argc, char** argv) {
   CK(hipStreamCreate(&st));
   const uintptr_t s = reinterpret_cast<uintptr_t>(d);
   for (int round = 0; round < 3; ++round) {
-    const double t[14] = {time_us<0, 4>(s, n, sink, st), time_us<0, 8>(s, n, sink, st), time_us<1, 4>(s, n, sink, st),
+    const double t[16] = {time_us<0, 4>(s, n, sink, st), time_us<0, 8>(s, n, sink, st), time_us<1, 4>(s, n, sink, st),
                           time_us<1, 8>(s, n, sink, st), time_us<2, 4>(s, n, sink, st), time_us<2, 8>(s, n, sink, st),
                           time_us<3, 4>(s, n, sink, st), time_us<3, 8>(s, n, sink, st), time_us<4, 4>(s, n, sink, st),
                           time_us<5, 4>(s, n, sink, st), time_us<6, 4>(s, n, sink, st), time_us<7, 4>(s, n, sink, st),
-                          time_us<8, 4>(s, n, sink, st), time_us<9, 4>(s, n, sink, st)};
-    const char* nm[14] = {"slot rows x4", "slot rows x8", "1KiB rows x4", "1KiB rows x8", "2-line slots x4",
+                          time_us<8, 4>(s, n, sink, st), time_us<9, 4>(s, n, sink, st), time_us<10, 4>(s, n, sink, st),
+                          time_us<11, 4>(s, n, sink, st)};
+    const char* nm[16] = {"slot rows x4", "slot rows x8", "1KiB rows x4", "1KiB rows x8", "2-line slots x4",
                           "2-line slots x8", "stream x4", "stream x8", "slot rows x4 rot/slot", "slot rows x4 rot/wave",
-                          "slot rows x4 rot/wg", "slot rows x4 half/wave", "slot rows x4 wg-window", "slot rows x4 wg-window il"};
-    for (int i = 0; i < 14; ++i)
+                          "slot rows x4 rot/wg", "slot rows x4 half/wave", "slot rows x4 wg-window",
+                          "slot rows x4 wg-window il", "slot rows x4 teams of 4", "slot rows x4 teams of 2"};
+    for (int i = 0; i < 16; ++i)
       std::printf("{\"round\": %d, \"mib\": %llu, \"pattern\": \"%s\", \"us\": %.2f, \"TBps\": %.3f}\n", round,
                   (unsigned long long)mib, nm[i], t[i], double(n) / (t[i] * 1e-6) / 1e12);
     std::fflush(stdout);
