@@ -288,7 +288,6 @@ int narrow_form(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes,
   if (c->kernel == 6) return 10;
   if (c->kernel == 7) return 11;
   if (c->kernel == 8) return 12;
-  if (c->kernel == 9) return 13;
   // 16-wave workgroups below 128 Ki blocks of <= 8 KiB (32 Ki blocks of 8-32 KiB), 8-wave ones from there on.  A
   // small batch gives each wave only a couple of 8-block groups, and more waves hide more of the launch/first-load
   // ramp (256 MiB of 4 KiB blocks: 16 waves +2-5 %); a large one streams better with 8 (1 GiB of 4 KiB blocks:
@@ -317,9 +316,6 @@ int narrow_form(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes,
 // 154.06 -- about 1 % at config 2, the time the loads cost; the rest of config 2's distance to the streaming read is not
 // in instruction count.  Bit 2 (no init load for init-less batches) measured nothing and is not shipped.
 constexpr uint32_t kClaimLean = 3;
-
-// Waves per team of crc32c_narrow_team_kernel (form 13).
-constexpr int kTeamWaves = 4;
 
 bool use_narrow(const kvsep_crc32c_ctx* c, uint64_t count, uint64_t total_bytes, uint64_t max_len) {
   if (max_len == 0 || max_len > 2 * kNarrowMax) return false;
@@ -568,7 +564,7 @@ int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, bool capt
     nv = diag_narrow_form(c, nv);  // KVSEP_DIAG build only
     a.hint = max_len;
     if (nv == 12 && a.hint > kCoopMaxLen) a.hint = kCoopMaxLen;  // its rows cover 4 KiB; longer blocks take its wide path
-    if (expect && (nv == 6 || nv == 9 || nv == 10 || nv == 11 || nv == 12 || nv == 13 || nv == 20)) {  // the shipped forms' verify
+    if (expect && (nv == 6 || nv == 9 || nv == 10 || nv == 11 || nv == 12 || nv == 20)) {  // the shipped forms' verify
       switch (nv) {
         case 9: crc32c_narrow_kernel<4, true, 512, true, true, LdsFull, true><<<grid, 512, 0, s>>>(a); break;
         case 10: crc32c_narrow_claim_kernel<4, 512, true, true, 8, kClaimLean><<<grid, 512, 0, s>>>(a); break;
@@ -577,7 +573,6 @@ int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, bool capt
           if (init) crc32c_narrow_coop_kernel<true, true><<<grid, 512, 0, s>>>(a);
           else crc32c_narrow_coop_kernel<true, false><<<grid, 512, 0, s>>>(a);
           break;
-        case 13: crc32c_narrow_team_kernel<4, kTeamWaves, true><<<grid, 512, 0, s>>>(a); break;
         case 20: crc32c_narrow_sorted_kernel<4, true, 1024, true><<<grid, 1024, 0, s>>>(a); break;
         default: crc32c_narrow_kernel<4, true, 1024, false, true, LdsFull, true><<<grid, 1024, 0, s>>>(a); break;
       }
@@ -599,7 +594,6 @@ int launch_batch_body(kvsep_crc32c_ctx* c, Scratch& sc, hipStream_t s, bool capt
         if (init) crc32c_narrow_coop_kernel<false, true><<<grid, 512, 0, s>>>(a);
         else crc32c_narrow_coop_kernel<false, false><<<grid, 512, 0, s>>>(a);
         break;
-      case 13: crc32c_narrow_team_kernel<4, kTeamWaves, false><<<grid, 512, 0, s>>>(a); break;
       case 20: crc32c_narrow_sorted_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
       default: crc32c_narrow_kernel<4, true, 1024><<<grid, 1024, 0, s>>>(a); break;
     }
@@ -740,7 +734,7 @@ int kvsep_crc32c_ctx_set_schedule(kvsep_crc32c_ctx* c, int dynamic) {
 }
 
 int kvsep_crc32c_ctx_set_kernel(kvsep_crc32c_ctx* c, int kernel) {
-  if (!c || kernel < 0 || kernel > 9) return set_err(KVSEP_EINVAL, "kernel must be 0..9");
+  if (!c || kernel < 0 || kernel > 8) return set_err(KVSEP_EINVAL, "kernel must be 0..8");
   std::lock_guard<std::mutex> g(c->mu);
   c->kernel = kernel;
   return KVSEP_OK;
@@ -953,7 +947,6 @@ const char* kvsep_crc32c_kernel_name(kvsep_crc32c_ctx* c, uint64_t count, uint64
   return nf == 20 ? "crc32c_narrow_sorted_kernel"
          : nf == 10 || nf == 11 ? "crc32c_narrow_claim_kernel"
          : nf == 12             ? "crc32c_narrow_coop_kernel"
-         : nf == 13             ? "crc32c_narrow_team_kernel"
                                 : "crc32c_narrow_kernel";
 }
 

@@ -280,14 +280,13 @@ class Context:
         _check(lib().kvsep_crc32c_ctx_set_schedule(self._h, v), "set_schedule")
 
     KERNELS = {"auto": 0, "wide": 1, "narrow": 2, "narrow16": 3, "narrow8": 4, "sorted": 5, "claim": 6, "claim16": 7,
-               "coop": 8, "team": 9}
+               "coop": 8}
 
     def set_kernel(self, kernel: str):
         """Kernel choice for unsplit batches (kvsep_crc32c_ctx_set_kernel): "auto" (default), "wide", or the narrow
         kernel whenever the max_len hint is <= 64 KiB ("narrow"; "narrow16" / "narrow8" pin its workgroup size,
         "sorted" its sorted-window form for ragged batches, "claim" / "claim16" its workgroup-run form with LDS claims,
-        8 / 16 lanes per block, "coop" the form whose 8 waves share each 8-block group, "team" the one whose waves work in pairs, each pair on
-        one group).  Never changes a result."""
+        8 / 16 lanes per block, "coop" the form whose 8 waves share each 8-block group).  Never changes a result."""
         _check(lib().kvsep_crc32c_ctx_set_kernel(self._h, self.KERNELS[kernel]), "set_kernel")
 
     def set_host_node(self, node: int):
