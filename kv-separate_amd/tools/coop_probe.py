@@ -87,14 +87,14 @@ def parity(ctxs):
 
 
 def graph_us(fn, ctx, reps=20):
-    fn()
+    fn(0)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
         with torch.cuda.graph(g, stream=s):
-            for _ in range(reps):
-                fn()
+            for i in range(reps):
+                fn(i)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     g.replay()
@@ -113,6 +113,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--lib", default=None)
+    ap.add_argument("--rotate", type=int, default=1,
+                    help="launch i reads copy i mod N of the batch (N copies: no launch finds the previous one's data "
+                         "in the 256 MB Infinity Cache once N x batch is well past it)")
     args = ap.parse_args()
     if args.lib:
         kvsep.LIB_PATH = os.path.abspath(args.lib)
@@ -126,8 +129,9 @@ def main():
         off, ln = W.uniform_layout(count, args.block)
         span = int(off[-1] + ln[-1])
         total = int(ln.sum())
-        data = torch.empty(span + 64, dtype=torch.uint8, device=dev)
-        kvsep.fill_splitmix64(data.data_ptr(), span, 1, 0)
+        datas = [torch.empty(span + 64, dtype=torch.uint8, device=dev) for _ in range(args.rotate)]
+        for data in datas:
+            kvsep.fill_splitmix64(data.data_ptr(), span, 1, 0)
         d_off, d_len = u64(off), u64(ln)
         outs = {k: torch.zeros(count, dtype=torch.int32, device=dev) for k in kernels}
         times = {k: [] for k in kernels}
@@ -135,16 +139,16 @@ def main():
             ctxs[k].reserve(count, total)
         for _ in range(args.rounds):
             for k in kernels:
-                times[k].append(graph_us(lambda k=k: ctxs[k].batch_device(
-                    data.data_ptr(), d_off, d_len, outs[k], count=count, total_bytes=total, max_len=args.block,
-                    stream=torch.cuda.current_stream()), ctxs[k]))
+                times[k].append(graph_us(lambda i, k=k: ctxs[k].batch_device(
+                    datas[i % args.rotate].data_ptr(), d_off, d_len, outs[k], count=count, total_bytes=total,
+                    max_len=args.block, stream=torch.cuda.current_stream()), ctxs[k]))
         ref = outs[kernels[0]].cpu()
         for k in kernels:
             t = sorted(times[k])
-            print(f"{mib:5d} MiB of {args.block}-B blocks {k:<8s} min {t[0]:8.2f} us  med {t[len(t) // 2]:8.2f} us"
+            print(f"{mib:5d} MiB of {args.block}-B blocks x{args.rotate} {k:<8s} min {t[0]:8.2f} us  med {t[len(t) // 2]:8.2f} us"
                   f"  {total / t[len(t) // 2] / 1e6:6.3f} TB/s  same={bool(torch.equal(outs[k].cpu(), ref))}",
                   flush=True)
-        del data, d_off, d_len, outs
+        del datas, d_off, d_len, outs
         torch.cuda.empty_cache()
     for c in ctxs.values():
         c.close()
